@@ -1,0 +1,60 @@
+# Builds (in-tree, so the .so files travel to the GPU box with gpurun):
+#   sycl-ray-tracing_amd/lib/librt_hip.so      product: gfx950 kernel + C ABI (hipcc)
+#   sycl-ray-tracing_amd/lib/librt_hostsim.so  CPU build of the same device code (tests only)
+#   oracle/liboracle.so                        CPU restatement oracle (tests / cpu_baseline only)
+#   build/libm_check                           libm restatement vs glibc checker
+#
+# Numerics: every object is built with -ffp-contract=off and without
+# -ffast-math / -march, because the reference (g++ -O2, baseline x86-64) never
+# fuses a*b+c and keeps IEEE division, sqrt, denormals and infinities.
+HIPCC ?= /opt/rocm/bin/hipcc
+CXX ?= g++
+ARCH ?= gfx950
+PKG := sycl-ray-tracing_amd
+SRC := $(PKG)/csrc
+LIB := $(PKG)/lib
+OBJ := build/obj
+
+CXXFLAGS := -std=c++17 -O2 -fPIC -ffp-contract=off -fno-fast-math -Wall -Wno-unused-function -Wno-unknown-pragmas
+HIPFLAGS := -std=c++17 -O3 -fPIC --offload-arch=$(ARCH) -ffp-contract=off -fno-fast-math \
+            -fno-gpu-flush-denormals-to-zero -fhip-fp32-correctly-rounded-divide-sqrt -Wall -Wno-unused-function -Wno-unknown-pragmas
+
+HDRS := $(wildcard $(SRC)/*.h) include/rt_hip.h
+
+all: $(LIB)/librt_hip.so $(LIB)/librt_hostsim.so oracle/liboracle.so build/libm_check
+
+$(OBJ)/%.host.o: $(SRC)/%.cpp $(HDRS)
+	@mkdir -p $(OBJ)
+	$(CXX) $(CXXFLAGS) -c $< -o $@
+
+$(OBJ)/rt_hostsim.o: $(SRC)/rt_hostsim.cpp $(HDRS)
+	@mkdir -p $(OBJ)
+	$(CXX) $(CXXFLAGS) -fopenmp -c $< -o $@
+
+$(OBJ)/rt_render.o: $(SRC)/rt_render.hip $(HDRS)
+	@mkdir -p $(OBJ)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(LIB)/librt_hip.so: $(OBJ)/rt_render.o $(OBJ)/rt_scene.host.o $(OBJ)/rt_capi_host.host.o
+	@mkdir -p $(LIB)
+	$(HIPCC) -shared --offload-arch=$(ARCH) -fPIC $^ -o $@
+
+$(LIB)/librt_hostsim.so: $(OBJ)/rt_hostsim.o $(OBJ)/rt_scene.host.o $(OBJ)/rt_capi_host.host.o
+	@mkdir -p $(LIB)
+	$(CXX) -shared -fopenmp $^ -o $@
+
+oracle/liboracle.so: oracle/cpu_oracle.cpp
+	$(MAKE) -C oracle liboracle.so
+
+build/libm_check: tests/native/libm_check.cpp $(SRC)/rt_libm.h $(SRC)/rt_fp.h
+	@mkdir -p build
+	$(CXX) -std=c++17 -O2 -fopenmp -ffp-contract=off -I$(SRC) $< -o $@ -lm
+
+# the reference build (container only; needs /root/reference)
+ref:
+	$(MAKE) -C oracle/ref OPT=-O2
+
+clean:
+	rm -rf $(OBJ) $(LIB) build/libm_check oracle/liboracle.so
+
+.PHONY: all ref clean

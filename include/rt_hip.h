@@ -1,0 +1,121 @@
+/* rt_hip.h — C ABI of librt_hip.so, the MI355X (gfx950) drop-in for the
+ * reference's render kernel.
+ *
+ * Reference interface replaced (TomClabault/SYCL-ray-tracing @ 2024-08-07):
+ *   class RenderKernel            include/render_kernel.h:21-96
+ *     RenderKernel(...)           include/render_kernel.h:24-46   -> rt_create + rt_set_scene
+ *                                                                   + rt_build_bvh / rt_set_bvh_preorder
+ *                                                                   + rt_set_env
+ *     set_camera(Camera)          include/render_kernel.h:48      -> rt_set_camera
+ *     render()                    include/render_kernel.h:57,
+ *                                 source/render_kernel.cpp:189-211 -> rt_render / rt_render_device
+ *     ray_trace_pixel(x, y)       include/render_kernel.h:56,
+ *                                 source/render_kernel.cpp:75-181  -> rt_render_pixels
+ *   BVH(triangles, 32, 8)         source/bvh.cpp:19-37            -> rt_build_bvh
+ *   BVH::intersect(ray, hit)      source/bvh.cpp:62-65            -> rt_intersect
+ *   Camera presets                source/camera.cpp:3-8           -> rt_camera_preset
+ *   Utils::parse_obj              source/utils.cpp:16-98          -> rt_mesh_load (+ rt_mesh_*)
+ *   Utils::compute_env_map_cdf    source/utils.cpp:126-142        -> rt_env_luminance_cdf
+ *
+ * Conventions: every function returns 0 (RT_OK) or a negative RT_ERR_*;
+ * rt_last_error() gives the message. Inputs are copied (the caller keeps
+ * ownership, like the reference's const std::vector& members). Calls are
+ * synchronous unless a stream is passed. One context per host thread.
+ * Buffer layouts are the reference's in-memory layouts:
+ *   triangles  float[n][9]  Triangle{Point m_a, m_b, m_c}       (triangle.h:67)
+ *   materials  float[m][10] SimpleMaterial{Color emission (rgba), Color diffuse (rgba),
+ *                           metalness, roughness}                (simple_material.h:6-13)
+ *   spheres    float[s][5]  Sphere{center xyz, radius, primitive_index (as float)} (sphere.h:7-59)
+ *   image      float[h][w][4] Image / Color RGBA                 (image.h:25-178)
+ *   view       float[16]    Transform::m row-major, + Camera::fov_dist (camera.h:38-40)
+ */
+#ifndef RT_HIP_H
+#define RT_HIP_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RT_OK 0
+#define RT_ERR_ARG (-1)
+#define RT_ERR_HIP (-2)
+#define RT_ERR_STATE (-3)
+#define RT_ERR_IO (-4)
+#define RT_ERR_NODEV (-5)
+
+typedef struct rt_context rt_context;
+typedef struct rt_mesh rt_mesh;
+
+/* ---------------------------------------------------------------- context */
+int rt_create(int device, rt_context** out);
+void rt_destroy(rt_context* ctx);
+const char* rt_last_error(const rt_context* ctx); /* ctx may be NULL: last global error */
+int rt_version(void);
+
+/* Scene buffers bound by the RenderKernel constructor (render_kernel.h:27-31). */
+int rt_set_scene(rt_context* ctx, const float* triangles, int n_triangles, const int* material_indices,
+                 int n_material_indices, const float* materials, int n_materials, const int* emissive_triangles,
+                 int n_emissive, const float* spheres, int n_spheres);
+
+/* BVH(&triangles, max_depth, leaf_max_obj_count): native octree build,
+ * bit-identical to bvh.h:55-125 (child-box quirk included). */
+int rt_build_bvh(rt_context* ctx, int max_depth, int leaf_max_obj_count);
+/* Drop-in for a reference-built BVH&: a pre-order walk of BVH::_root, per node
+ * {int is_leaf, int n, int tris[n], float min[3], max[3], d_near[7], d_far[7]},
+ * children 0..7 after each internal node (INTEGRATION.md shows the walker). */
+int rt_set_bvh_preorder(rt_context* ctx, const void* dump, long bytes);
+/* Pre-order dump of the context's octree in the same format; returns the size. */
+long rt_bvh_dump(const rt_context* ctx, void* buf, long capacity);
+/* info[0..4] = octree nodes, GPU child records, triangles, max depth, GPU bytes */
+int rt_bvh_info(const rt_context* ctx, long* info);
+
+/* skysphere Image + env_map_cdf (render_kernel.h:33-34). `pixels` has
+ * `channels` (3 or 4) floats per texel, row 0 first (as read_image_float
+ * leaves it). cdf may be NULL: computed exactly like compute_env_map_cdf. */
+int rt_set_env(rt_context* ctx, const float* pixels, int width, int height, int channels, const float* cdf);
+
+/* RenderKernel::set_camera. */
+int rt_set_camera(rt_context* ctx, const float view[16], float fov_dist);
+
+/* RenderKernel::render(): fb_rgba (host, w*h*4) is read (accumulated into)
+ * and overwritten with the tone-mapped result, exactly as the reference
+ * mutates its Image&. */
+int rt_render(rt_context* ctx, int width, int height, int samples, int max_bounces, float* fb_rgba);
+
+/* Device-resident render for benchmarking / multi-GPU sharding: renders image
+ * rows y = row_offset + j*row_stride (j = 0..) into d_fb (device, rows_local*w*4
+ * floats, row j of the shard at offset j*w*4). stream may be NULL (default). */
+int rt_render_device(rt_context* ctx, int width, int height, int samples, int max_bounces, void* d_fb,
+                     int row_offset, int row_stride, void* stream);
+
+/* ray_trace_pixel for a list of n pixels xy[n][2]: rgba[n][4] holds each
+ * pixel's framebuffer value on entry and the tone-mapped value on return. */
+int rt_render_pixels(rt_context* ctx, int width, int height, int samples, int max_bounces, const int* xy, int n,
+                     float* rgba);
+
+/* BVH::intersect + sphere loop (INTERSECT_SCENE) for n rays rays[n][6]
+ * (origin, direction); out[n][11] = {found, primitive, t, point[3],
+ * normal[3], u, v} with u = v = -1 (unused downstream). */
+int rt_intersect(rt_context* ctx, const float* rays, int n, void* out);
+
+/* Counters of the last render when enabled (RT_STAT_* order, rt_device.h). */
+int rt_set_stats(rt_context* ctx, int enabled);
+int rt_get_stats(const rt_context* ctx, unsigned long long* out, int n);
+/* Average duration (ms) of the last render kernel measured with HIP events. */
+double rt_last_kernel_ms(const rt_context* ctx);
+
+/* ------------------------------------------------- host helpers (no GPU) */
+int rt_mesh_load(const char* obj_path, rt_mesh** out);
+int rt_mesh_counts(const rt_mesh* m, int* n_triangles, int* n_materials, int* n_emissive);
+int rt_mesh_copy(const rt_mesh* m, float* triangles, int* material_indices, float* materials, int* emissive);
+void rt_mesh_free(rt_mesh* m);
+int rt_camera_preset(const char* name, float view[16], float* fov_dist);
+int rt_env_luminance_cdf(const float* pixels, int width, int height, int channels, float* lum, float* cdf);
+/* Octree of a triangle buffer without a device (parity tests). */
+long rt_octree_dump(const float* triangles, int n_triangles, int max_depth, int leaf_max, void* buf, long capacity);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* RT_HIP_H */

@@ -280,6 +280,16 @@ int main(int argc, char** argv)
         if (argc < (cmd == "render" ? 10 : 11)) return 2;
         Scene s;
         load_scene(s, argv[2], argv[3]);
+        // optional material override (Cook-Torrance sweep, BASELINE config 5):
+        // env RT_MAT_OVERRIDE="index:metalness:roughness"
+        if (const char* mo = std::getenv("RT_MAT_OVERRIDE")) {
+            int mi;
+            float me, ro;
+            if (std::sscanf(mo, "%d:%f:%f", &mi, &me, &ro) == 3 && mi >= 0 && mi < (int)s.obj.materials.size()) {
+                s.obj.materials[mi].metalness = me;
+                s.obj.materials[mi].roughness = ro;
+            }
+        }
         Camera cam = camera_by_name(argv[4]);
         const int W = std::atoi(argv[5]), H = std::atoi(argv[6]);
         const int spp = std::atoi(argv[7]), bounces = std::atoi(argv[8]);

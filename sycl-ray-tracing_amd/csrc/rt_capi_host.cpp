@@ -1,0 +1,346 @@
+// rt_capi_host.cpp — the backend-independent half of the C ABI
+// (include/rt_hip.h): argument checking, host scene preparation, host
+// helpers. The compute half lives in rt_render.hip (gfx950).
+#include <cstring>
+#include <mutex>
+
+#include "rt_context.h"
+
+namespace {
+std::mutex g_err_mu;
+std::string g_err;
+void set_global_err(const std::string& m)
+{
+    std::lock_guard<std::mutex> lk(g_err_mu);
+    g_err = m;
+}
+}  // namespace
+
+int rt_fail(rt_context* ctx, int code, const std::string& msg)
+{
+    if (ctx) ctx->err = msg;
+    set_global_err(msg);
+    return code;
+}
+
+RtSceneView rt_host_view(const rt_context* c)
+{
+    RtSceneView v{};
+    v.nodes = c->flat.nodes.data();
+    v.tri4 = c->flat.tri4.data();
+    v.prim2k = c->flat.prim2k.data();
+    v.mat_idx = c->mat_idx.data();
+    v.mats = c->mats.data();
+    v.emissive = c->emissive.data();
+    v.spheres = c->spheres.data();
+    v.env = c->env.data();
+    v.env_lum = c->env_lum.data();
+    v.cdf = c->cdf.data();
+    v.n_emissive = (int)c->emissive.size();
+    v.n_spheres = (int)(c->spheres.size() / 2);
+    v.ew = c->ew;
+    v.eh = c->eh;
+    v.n_tris = (int)(c->tris.size() / 9);
+    return v;
+}
+
+extern "C" {
+
+int rt_version(void) { return 10000; }
+
+const char* rt_last_error(const rt_context* ctx)
+{
+    if (ctx) return ctx->err.c_str();
+    std::lock_guard<std::mutex> lk(g_err_mu);
+    static thread_local std::string copy;
+    copy = g_err;
+    return copy.c_str();
+}
+
+int rt_create(int device, rt_context** out)
+{
+    if (!out) return rt_fail(nullptr, RT_ERR_ARG, "rt_create: out is NULL");
+    *out = nullptr;
+    rt_context* c = new rt_context();
+    c->device = device;
+    int r = rt_backend_create(c);
+    if (r) {
+        set_global_err(c->err);
+        delete c;
+        return r;
+    }
+    *out = c;
+    return RT_OK;
+}
+
+void rt_destroy(rt_context* ctx)
+{
+    if (!ctx) return;
+    rt_backend_destroy(ctx);
+    delete ctx;
+}
+
+int rt_set_scene(rt_context* c, const float* triangles, int n, const int* material_indices, int n_mi,
+                 const float* materials, int n_mats, const int* emissive, int n_em, const float* spheres, int n_sph)
+{
+    if (!c) return rt_fail(nullptr, RT_ERR_ARG, "rt_set_scene: ctx is NULL");
+    if (n < 0 || (n > 0 && !triangles) || n_mats <= 0 || !materials || n_mi < n || (n_mi > 0 && !material_indices) ||
+        n_em < 0 || (n_em > 0 && !emissive) || n_sph < 0 || (n_sph > 0 && !spheres))
+        return rt_fail(c, RT_ERR_ARG, "rt_set_scene: bad buffer sizes");
+    for (int i = 0; i < n_mi; i++)
+        if (material_indices[i] < 0 || material_indices[i] >= n_mats)
+            return rt_fail(c, RT_ERR_ARG, "rt_set_scene: material index out of range");
+    for (int i = 0; i < n_em; i++)
+        if (emissive[i] < 0 || emissive[i] >= n) return rt_fail(c, RT_ERR_ARG, "rt_set_scene: emissive id out of range");
+    for (int i = 0; i < n_sph; i++) {
+        const int prim = (int)spheres[5 * i + 4];
+        if (prim < 0 || prim >= n_mi)
+            return rt_fail(c, RT_ERR_ARG, "rt_set_scene: sphere primitive index has no material index");
+    }
+    c->tris.assign(triangles, triangles + 9 * (size_t)n);
+    c->mat_idx.assign(material_indices, material_indices + n_mi);
+    c->mats.resize(n_mats);
+    for (int i = 0; i < n_mats; i++) {
+        const float* p = materials + 10 * (size_t)i;
+        c->mats[i] = RtMat{p[0], p[1], p[2], p[8], p[4], p[5], p[6], p[9]};
+    }
+    c->emissive.assign(emissive, emissive + n_em);
+    c->spheres.clear();
+    for (int i = 0; i < n_sph; i++) {
+        const float* p = spheres + 5 * (size_t)i;
+        float4_ a{p[0], p[1], p[2], p[3]}, b{0, 0, 0, 0};
+        const int prim = (int)p[4];
+        std::memcpy(&b.x, &prim, 4);
+        c->spheres.push_back(a);
+        c->spheres.push_back(b);
+    }
+    c->have_scene = true;
+    c->have_bvh = false;
+    c->dirty = true;
+    return RT_OK;
+}
+
+int rt_build_bvh(rt_context* c, int max_depth, int leaf_max)
+{
+    if (!c || !c->have_scene) return rt_fail(c, RT_ERR_STATE, "rt_build_bvh: no scene");
+    if (max_depth > 32 || max_depth < -1 || leaf_max < 1)
+        return rt_fail(c, RT_ERR_ARG, "rt_build_bvh: max_depth must be -1..32 (device stack bound), leaf_max >= 1");
+    const int n = (int)(c->tris.size() / 9);
+    rt::build_octree(c->tris.data(), n, max_depth, leaf_max, c->octree);
+    rt::flatten_octree(c->octree, c->tris.data(), n, c->flat);
+    if (c->flat.max_depth > 32) return rt_fail(c, RT_ERR_ARG, "rt_build_bvh: octree deeper than 32");
+    c->have_bvh = true;
+    c->dirty = true;
+    return RT_OK;
+}
+
+int rt_set_bvh_preorder(rt_context* c, const void* dump, long bytes)
+{
+    if (!c || !c->have_scene) return rt_fail(c, RT_ERR_STATE, "rt_set_bvh_preorder: no scene");
+    if (!dump || bytes <= 0) return rt_fail(c, RT_ERR_ARG, "rt_set_bvh_preorder: empty dump");
+    rt::Octree t;
+    if (rt::octree_from_dump((const char*)dump, (size_t)bytes, t))
+        return rt_fail(c, RT_ERR_ARG, "rt_set_bvh_preorder: malformed pre-order dump");
+    const int n = (int)(c->tris.size() / 9);
+    for (const auto& nd : t.pool)
+        for (int id : nd.tris)
+            if (id < 0 || id >= n) return rt_fail(c, RT_ERR_ARG, "rt_set_bvh_preorder: triangle id out of range");
+    c->octree = std::move(t);
+    rt::flatten_octree(c->octree, c->tris.data(), n, c->flat);
+    if (c->flat.max_depth > 32) return rt_fail(c, RT_ERR_ARG, "rt_set_bvh_preorder: octree deeper than 32");
+    c->have_bvh = true;
+    c->dirty = true;
+    return RT_OK;
+}
+
+long rt_bvh_dump(const rt_context* c, void* buf, long cap)
+{
+    if (!c || !c->have_bvh) return RT_ERR_STATE;
+    std::vector<char> d = rt::dump_octree(c->octree);
+    if (buf && cap >= (long)d.size()) std::memcpy(buf, d.data(), d.size());
+    return (long)d.size();
+}
+
+int rt_bvh_info(const rt_context* c, long* info)
+{
+    if (!c || !c->have_bvh || !info) return RT_ERR_STATE;
+    info[0] = (long)c->octree.pool.size();
+    info[1] = (long)c->flat.nodes.size();
+    info[2] = (long)(c->tris.size() / 9);
+    info[3] = c->flat.max_depth;
+    info[4] = (long)(c->flat.nodes.size() * sizeof(RtNode) + c->flat.tri4.size() * sizeof(float4_) +
+                     c->flat.prim2k.size() * 4);
+    return RT_OK;
+}
+
+int rt_set_env(rt_context* c, const float* px, int w, int h, int ch, const float* cdf)
+{
+    if (!c) return rt_fail(nullptr, RT_ERR_ARG, "rt_set_env: ctx is NULL");
+    if (!px || w <= 0 || h <= 0 || (ch != 3 && ch != 4)) return rt_fail(c, RT_ERR_ARG, "rt_set_env: bad image");
+    const size_t n = (size_t)w * h;
+    c->ew = w;
+    c->eh = h;
+    c->env.resize(n);
+    for (size_t i = 0; i < n; i++) c->env[i] = float4_{px[ch * i], px[ch * i + 1], px[ch * i + 2], 0.0f};
+    c->env_lum.resize(n);
+    c->cdf.resize(n);
+    rt::env_luminance_cdf(px, w, h, ch, c->env_lum.data(), c->cdf.data());
+    if (cdf) c->cdf.assign(cdf, cdf + n);
+    c->have_env = true;
+    c->dirty = true;
+    return RT_OK;
+}
+
+int rt_set_camera(rt_context* c, const float view[16], float fov_dist)
+{
+    if (!c || !view) return rt_fail(c, RT_ERR_ARG, "rt_set_camera: bad arguments");
+    std::memcpy(c->cam.m, view, 64);
+    c->cam.fov_dist = fov_dist;
+    c->have_cam = true;
+    return RT_OK;
+}
+
+static int check_ready(rt_context* c, int w, int h, int spp, int bounces)
+{
+    if (!c) return rt_fail(nullptr, RT_ERR_ARG, "ctx is NULL");
+    if (!c->have_scene || !c->have_bvh) return rt_fail(c, RT_ERR_STATE, "scene/BVH not set");
+    if (!c->have_env) return rt_fail(c, RT_ERR_STATE, "environment map not set");
+    if (!c->have_cam) return rt_fail(c, RT_ERR_STATE, "camera not set");
+    if (w <= 0 || h <= 0 || spp <= 0 || bounces < 0) return rt_fail(c, RT_ERR_ARG, "bad render size");
+    // the reference seeds with the int 31 + x*y*spp (render_kernel.cpp:77)
+    if ((double)(w - 1) * (double)(h - 1) * (double)spp + 31.0 > 2147483647.0)
+        return rt_fail(c, RT_ERR_ARG, "31 + x*y*spp overflows int (reference seed)");
+    if (c->dirty) {
+        int r = rt_backend_upload(c);
+        if (r) return r;
+        c->dirty = false;
+    }
+    return RT_OK;
+}
+
+int rt_render(rt_context* c, int w, int h, int spp, int bounces, float* fb)
+{
+    if (int r = check_ready(c, w, h, spp, bounces)) return r;
+    if (!fb) return rt_fail(c, RT_ERR_ARG, "rt_render: fb is NULL");
+    return rt_backend_render(c, w, h, spp, bounces, fb, nullptr, 0, 1, nullptr);
+}
+
+int rt_render_device(rt_context* c, int w, int h, int spp, int bounces, void* d_fb, int row_offset, int row_stride,
+                     void* stream)
+{
+    if (int r = check_ready(c, w, h, spp, bounces)) return r;
+    if (!d_fb || row_stride <= 0 || row_offset < 0 || row_offset >= row_stride)
+        return rt_fail(c, RT_ERR_ARG, "rt_render_device: bad shard");
+    return rt_backend_render(c, w, h, spp, bounces, nullptr, d_fb, row_offset, row_stride, stream);
+}
+
+int rt_render_pixels(rt_context* c, int w, int h, int spp, int bounces, const int* xy, int n, float* rgba)
+{
+    if (int r = check_ready(c, w, h, spp, bounces)) return r;
+    if (n < 0 || (n > 0 && (!xy || !rgba))) return rt_fail(c, RT_ERR_ARG, "rt_render_pixels: bad buffers");
+    for (int i = 0; i < n; i++)
+        if (xy[2 * i] < 0 || xy[2 * i] >= w || xy[2 * i + 1] < 0 || xy[2 * i + 1] >= h)
+            return rt_fail(c, RT_ERR_ARG, "rt_render_pixels: pixel outside the image");
+    if (n == 0) return RT_OK;
+    return rt_backend_render_pixels(c, w, h, spp, bounces, xy, n, rgba);
+}
+
+int rt_intersect(rt_context* c, const float* rays, int n, void* out)
+{
+    if (!c || !c->have_scene || !c->have_bvh) return rt_fail(c, RT_ERR_STATE, "rt_intersect: scene/BVH not set");
+    if (n < 0 || (n > 0 && (!rays || !out))) return rt_fail(c, RT_ERR_ARG, "rt_intersect: bad buffers");
+    if (n == 0) return RT_OK;
+    if (c->dirty) {
+        if (!c->have_env) {
+            // a 1x1 black env keeps the device view valid for ray queries
+            const float z[3] = {0, 0, 0};
+            rt_set_env(c, z, 1, 1, 3, nullptr);
+        }
+        int r = rt_backend_upload(c);
+        if (r) return r;
+        c->dirty = false;
+    }
+    return rt_backend_intersect(c, rays, n, out);
+}
+
+int rt_set_stats(rt_context* c, int enabled)
+{
+    if (!c) return RT_ERR_ARG;
+    c->stats_enabled = enabled != 0;
+    return RT_OK;
+}
+
+int rt_get_stats(const rt_context* c, unsigned long long* out, int n)
+{
+    if (!c || !out) return RT_ERR_ARG;
+    for (int i = 0; i < n && i < RT_STAT_COUNT; i++) out[i] = c->stats[i];
+    return RT_OK;
+}
+
+double rt_last_kernel_ms(const rt_context* c) { return c ? c->last_kernel_ms : -1.0; }
+
+// ------------------------------------------------------------- host helpers
+struct rt_mesh {
+    rt::Mesh m;
+};
+
+int rt_mesh_load(const char* path, rt_mesh** out)
+{
+    if (!path || !out) return rt_fail(nullptr, RT_ERR_ARG, "rt_mesh_load: bad arguments");
+    *out = nullptr;
+    rt_mesh* m = new rt_mesh();
+    std::string err;
+    int r = rt::load_obj(path, m->m, err);
+    if (r) {
+        delete m;
+        return rt_fail(nullptr, RT_ERR_IO, "rt_mesh_load: " + err);
+    }
+    *out = m;
+    return RT_OK;
+}
+
+int rt_mesh_counts(const rt_mesh* m, int* nt, int* nm, int* ne)
+{
+    if (!m) return RT_ERR_ARG;
+    if (nt) *nt = m->m.ntris();
+    if (nm) *nm = (int)(m->m.mats.size() / 10);
+    if (ne) *ne = (int)m->m.emissive.size();
+    return RT_OK;
+}
+
+int rt_mesh_copy(const rt_mesh* m, float* tris, int* mi, float* mats, int* em)
+{
+    if (!m) return RT_ERR_ARG;
+    if (tris) std::memcpy(tris, m->m.tris.data(), m->m.tris.size() * 4);
+    if (mi) std::memcpy(mi, m->m.mat_idx.data(), m->m.mat_idx.size() * 4);
+    if (mats) std::memcpy(mats, m->m.mats.data(), m->m.mats.size() * 4);
+    if (em) std::memcpy(em, m->m.emissive.data(), m->m.emissive.size() * 4);
+    return RT_OK;
+}
+
+void rt_mesh_free(rt_mesh* m) { delete m; }
+
+int rt_camera_preset(const char* name, float view[16], float* fov_dist)
+{
+    if (!name || !view || !fov_dist) return RT_ERR_ARG;
+    return rt::camera_preset(name, view, fov_dist) ? rt_fail(nullptr, RT_ERR_ARG, "unknown camera preset") : RT_OK;
+}
+
+int rt_env_luminance_cdf(const float* px, int w, int h, int ch, float* lum, float* cdf)
+{
+    if (!px || w <= 0 || h <= 0 || (ch != 3 && ch != 4) || !lum || !cdf) return RT_ERR_ARG;
+    rt::env_luminance_cdf(px, w, h, ch, lum, cdf);
+    return RT_OK;
+}
+
+long rt_octree_dump(const float* tris, int n, int max_depth, int leaf_max, void* buf, long cap)
+{
+    if (!tris || n < 0) return RT_ERR_ARG;
+    rt::Octree t;
+    rt::build_octree(tris, n, max_depth, leaf_max, t);
+    std::vector<char> d = rt::dump_octree(t);
+    if (buf && cap >= (long)d.size()) std::memcpy(buf, d.data(), d.size());
+    return (long)d.size();
+}
+
+}  // extern "C"

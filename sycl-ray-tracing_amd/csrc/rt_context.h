@@ -1,0 +1,57 @@
+// rt_context.h — the state behind an rt_context* (include/rt_hip.h).
+//
+// Host-side scene state is shared; the compute backend (rt_render.hip for
+// gfx950, rt_hostsim.cpp for the CPU debugging build used by the CPU test
+// suite) implements the rt_backend_* hooks.
+#pragma once
+
+#include <string>
+#include <vector>
+
+#include "../../include/rt_hip.h"
+#include "rt_device.h"
+#include "rt_scene.h"
+
+struct rt_context {
+    int device = 0;
+    std::string err;
+
+    // RenderKernel constructor inputs (render_kernel.h:27-34)
+    std::vector<float> tris;      // [N][9]
+    std::vector<int32_t> mat_idx; // >= N entries (spheres append theirs)
+    std::vector<RtMat> mats;
+    std::vector<int32_t> emissive;
+    std::vector<float4_> spheres; // 2 records per sphere
+    bool have_scene = false;
+
+    rt::Octree octree;
+    rt::FlatBvh flat;
+    bool have_bvh = false;
+
+    std::vector<float4_> env;     // RGBA, alpha 0
+    std::vector<float> env_lum, cdf;
+    int ew = 0, eh = 0;
+    bool have_env = false;
+
+    RtCamera cam{};
+    bool have_cam = false;
+
+    bool stats_enabled = false;
+    unsigned long long stats[RT_STAT_COUNT] = {};
+    double last_kernel_ms = 0.0;
+
+    bool dirty = true;            // host state changed since the last upload
+    void* backend = nullptr;
+};
+
+// ---- backend hooks
+int rt_backend_create(rt_context* ctx);
+void rt_backend_destroy(rt_context* ctx);
+int rt_backend_upload(rt_context* ctx);
+int rt_backend_render(rt_context* ctx, int w, int h, int spp, int bounces, float* host_fb, void* dev_fb, int row_offset,
+                      int row_stride, void* stream);
+int rt_backend_render_pixels(rt_context* ctx, int w, int h, int spp, int bounces, const int* xy, int n, float* rgba);
+int rt_backend_intersect(rt_context* ctx, const float* rays, int n, void* out);
+
+int rt_fail(rt_context* ctx, int code, const std::string& msg);
+RtSceneView rt_host_view(const rt_context* ctx);  // host-memory view (hostsim)

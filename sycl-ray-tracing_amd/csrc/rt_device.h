@@ -1,0 +1,71 @@
+// rt_device.h — data layout shared by the host flattener and the gfx950
+// kernel (plain structs, no HIP types, so g++ can include it too).
+//
+// HBM layout:
+//   RtNode   64 B  one child record: the 7-DOP slabs of a non-empty octree
+//                  node + where its contents are. The children of an
+//                  internal node occupy `cnt` consecutive records starting at
+//                  `ref`, in child-index order (empty children are dropped;
+//                  they can never be hit by a non-NaN ray).
+//                  Record 0 is the root.
+//   tri4     48 B  per triangle, in leaf order: {a.xyz, prim}, {e1.xyz, 0},
+//                  {e2.xyz, 0} with e1 = b - a, e2 = c - a computed exactly
+//                  as Triangle::intersect does (triangle.h:21-22).
+//   RtMat    32 B  SimpleMaterial {emission.rgb, metalness, diffuse.rgb, roughness}.
+//   env      16 B  per texel RGBA (alpha 0), plus f32 luminance and CDF.
+#pragma once
+
+#include <stdint.h>
+
+struct alignas(16) float4_ {
+    float x, y, z, w;
+};
+
+#define RT_LEAF_BIT 0x80000000u
+
+struct alignas(16) RtNode {
+    float dn[7];
+    float df[7];
+    uint32_t ref;  // internal: first child record; leaf: first triangle (leaf order)
+    uint32_t cnt;  // internal: number of child records (1..8); leaf: RT_LEAF_BIT | triangle count
+};
+static_assert(sizeof(RtNode) == 64, "RtNode must be 64 B");
+
+struct alignas(16) RtMat {
+    float er, eg, eb, metalness;
+    float dr, dg, db, roughness;
+};
+
+struct RtSceneView {
+    const RtNode* nodes;
+    const float4_* tri4;
+    const int32_t* prim2k;
+    const int32_t* mat_idx;
+    const RtMat* mats;
+    const int32_t* emissive;
+    const float4_* spheres;  // 2 records each: {c.xyz, r}, {prim bits, 0, 0, 0}
+    const float4_* env;
+    const float* env_lum;
+    const float* cdf;
+    int32_t n_emissive, n_spheres, ew, eh;
+    int32_t n_tris, pad0, pad1, pad2;
+};
+
+struct RtCamera {
+    float m[16];
+    float fov_dist;
+};
+
+// Per-launch counters (stats build): rays traced, child-volume tests,
+// triangle tests, leaf visits, material fetches, env texel fetches, CDF probes.
+enum {
+    RT_STAT_RAYS = 0,
+    RT_STAT_VOL,
+    RT_STAT_TRI,
+    RT_STAT_LEAF,
+    RT_STAT_MAT,
+    RT_STAT_ENV,
+    RT_STAT_CDF,
+    RT_STAT_HEAP_SLOW,
+    RT_STAT_COUNT
+};

@@ -14,7 +14,7 @@
 #include <hip/hip_runtime.h>
 #define RT_HD __host__ __device__ __forceinline__
 #else
-#define RT_HD static inline
+#define RT_HD inline
 #endif
 
 RT_HD uint32_t rt_asuint(float f) { return __builtin_bit_cast(uint32_t, f); }

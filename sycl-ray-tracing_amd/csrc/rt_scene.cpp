@@ -1,0 +1,559 @@
+// rt_scene.cpp — host scene preparation (see rt_scene.h). Compiled with
+// -ffp-contract=off and no -march so every float operation is a single IEEE
+// SSE operation, as in the reference build.
+#include "rt_scene.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <sstream>
+#include <unordered_map>
+
+namespace rt {
+
+// ======================================================================= OBJ
+namespace {
+
+struct MtlMat {
+    float kd[3] = {0, 0, 0}, ke[3] = {0, 0, 0};
+    float pr = 0.0f, pm = 0.0f;
+    int illum = 0;
+};
+
+bool read_file(const std::string& path, std::string& out)
+{
+    std::ifstream f(path, std::ios::binary);
+    if (!f) return false;
+    std::ostringstream ss;
+    ss << f.rdbuf();
+    out = ss.str();
+    return true;
+}
+
+inline const char* skip_ws(const char* p, const char* e)
+{
+    while (p < e && (*p == ' ' || *p == '\t' || *p == '\r')) p++;
+    return p;
+}
+
+// Reads one token as float with correct rounding (strtof), like rapidobj's
+// parser does for the "%f" decimal strings in these files.
+inline bool read_float(const char*& p, const char* e, float& v)
+{
+    p = skip_ws(p, e);
+    if (p >= e || *p == '\n') return false;
+    char* end;
+    v = std::strtof(p, &end);
+    if (end == p) return false;
+    p = end;
+    return true;
+}
+
+std::string dirname_of(const std::string& path)
+{
+    size_t s = path.find_last_of('/');
+    return s == std::string::npos ? std::string(".") : path.substr(0, s);
+}
+
+int load_mtl(const std::string& path, std::vector<MtlMat>& mats, std::unordered_map<std::string, int>& names,
+             std::string& err)
+{
+    std::string text;
+    if (!read_file(path, text)) {
+        err = "cannot read material library " + path;
+        return -2;
+    }
+    std::istringstream in(text);
+    std::string line;
+    MtlMat* cur = nullptr;
+    while (std::getline(in, line)) {
+        if (!line.empty() && line.back() == '\r') line.pop_back();
+        const char* p = line.c_str();
+        const char* e = p + line.size();
+        p = skip_ws(p, e);
+        if (p >= e || *p == '#') continue;
+        const char* k = p;
+        while (p < e && *p != ' ' && *p != '\t') p++;
+        std::string key(k, p);
+        if (key == "newmtl") {
+            p = skip_ws(p, e);
+            std::string name(p, e);
+            while (!name.empty() && (name.back() == ' ' || name.back() == '\t')) name.pop_back();
+            names[name] = (int)mats.size();
+            mats.emplace_back();
+            cur = &mats.back();
+        } else if (!cur) {
+            continue;
+        } else if (key == "Kd" || key == "Ke") {
+            float* dst = key == "Kd" ? cur->kd : cur->ke;
+            float v[3];
+            int n = 0;
+            while (n < 3 && read_float(p, e, v[n])) n++;
+            if (n == 1) v[1] = v[2] = v[0];
+            if (n >= 1) std::memcpy(dst, v, sizeof v);
+        } else if (key == "Pr") {
+            read_float(p, e, cur->pr);
+        } else if (key == "Pm") {
+            read_float(p, e, cur->pm);
+        } else if (key == "illum") {
+            cur->illum = std::atoi(skip_ws(p, e));
+        }
+    }
+    return 0;
+}
+
+// OBJ index: 1-based, negative = relative to the current end.
+inline bool read_index(const char*& p, const char* e, int nverts, int& out)
+{
+    p = skip_ws(p, e);
+    if (p >= e || *p == '\n' || *p == '#') return false;
+    char* end;
+    long v = std::strtol(p, &end, 10);
+    if (end == p) return false;
+    p = end;
+    while (p < e && *p != ' ' && *p != '\t' && *p != '\r') p++;  // skip /vt/vn
+    out = v > 0 ? (int)(v - 1) : (int)(nverts + v);
+    return true;
+}
+
+}  // namespace
+
+int load_obj(const std::string& path, Mesh& out, std::string& err)
+{
+    std::string text;
+    if (!read_file(path, text)) {
+        err = "cannot read " + path;
+        return -1;
+    }
+    std::vector<float> pos;
+    pos.reserve(text.size() / 8);
+    std::vector<MtlMat> mtl;
+    std::unordered_map<std::string, int> names;
+    int cur_mat = -1;
+    out = Mesh();
+    const char* p = text.data();
+    const char* end = p + text.size();
+    std::vector<int> face;
+    while (p < end) {
+        const char* le = (const char*)std::memchr(p, '\n', end - p);
+        if (!le) le = end;
+        const char* q = skip_ws(p, le);
+        if (q + 1 < le && q[0] == 'v' && (q[1] == ' ' || q[1] == '\t')) {
+            q += 1;
+            float v[3];
+            for (int i = 0; i < 3; i++)
+                if (!read_float(q, le, v[i])) {
+                    err = "bad vertex line";
+                    return -3;
+                }
+            pos.insert(pos.end(), v, v + 3);
+        } else if (q + 1 < le && q[0] == 'f' && (q[1] == ' ' || q[1] == '\t')) {
+            q += 1;
+            face.clear();
+            int idx;
+            const int nv = (int)(pos.size() / 3);
+            while (read_index(q, le, nv, idx)) face.push_back(idx);
+            if (face.size() < 3) {
+                err = "face with fewer than 3 vertices";
+                return -3;
+            }
+            for (int i : face)
+                if (i < 0 || i >= nv) {
+                    err = "face index out of range";
+                    return -3;
+                }
+            auto emit = [&](int i0, int i1, int i2) {
+                const int id[3] = {i0, i1, i2};
+                for (int k = 0; k < 3; k++) out.tris.insert(out.tris.end(), &pos[3 * id[k]], &pos[3 * id[k]] + 3);
+                out.mat_idx.push_back(cur_mat + 1);  // utils.cpp:51-56
+                bool em = false;
+                if (cur_mat >= 0) {
+                    const float* ke = mtl[cur_mat].ke;
+                    em = ke[0] > 0 || ke[1] > 0 || ke[2] > 0;  // utils.cpp:58-69
+                }
+                if (em) out.emissive.push_back(out.ntris() - 1);
+            };
+            if (face.size() == 3) {
+                emit(face[0], face[1], face[2]);
+            } else if (face.size() == 4) {
+                // rapidobj::Triangulate quad rule (rapidobj.hpp:7164-7225): split on the
+                // shorter diagonal, d02 < d13 computed in float.
+                const float* P0 = &pos[3 * face[0]];
+                const float* P1 = &pos[3 * face[1]];
+                const float* P2 = &pos[3 * face[2]];
+                const float* P3 = &pos[3 * face[3]];
+                float e02x = P0[0] - P2[0], e02y = P0[1] - P2[1], e02z = P0[2] - P2[2];
+                float e13x = P1[0] - P3[0], e13y = P1[1] - P3[1], e13z = P1[2] - P3[2];
+                float d02 = e02x * e02x + e02y * e02y + e02z * e02z;
+                float d13 = e13x * e13x + e13y * e13y + e13z * e13z;
+                bool less = d02 < d13;
+                emit(face[0], face[1], less ? face[2] : face[3]);
+                emit(less ? face[0] : face[1], face[2], face[3]);
+            } else {
+                err = "polygons with more than 4 vertices are not supported (rapidobj earcut path)";
+                return -4;
+            }
+        } else if (q + 6 < le && std::strncmp(q, "usemtl", 6) == 0 && (q[6] == ' ' || q[6] == '\t')) {
+            q = skip_ws(q + 6, le);
+            std::string name(q, le);
+            while (!name.empty() && (name.back() == ' ' || name.back() == '\t' || name.back() == '\r')) name.pop_back();
+            auto it = names.find(name);
+            cur_mat = it == names.end() ? -1 : it->second;
+        } else if (q + 6 < le && std::strncmp(q, "mtllib", 6) == 0 && (q[6] == ' ' || q[6] == '\t')) {
+            q = skip_ws(q + 6, le);
+            std::string name(q, le);
+            while (!name.empty() && (name.back() == ' ' || name.back() == '\t' || name.back() == '\r')) name.pop_back();
+            int r = load_mtl(dirname_of(path) + "/" + name, mtl, names, err);
+            if (r) return r;
+        }
+        p = le + 1;
+    }
+    // SimpleMaterial list (utils.cpp:73-95)
+    auto push_mat = [&](float er, float eg, float eb, float dr, float dg, float db, float metal, float rough) {
+        const float m[10] = {er, eg, eb, 1.0f, dr, dg, db, 1.0f, metal, rough};
+        out.mats.insert(out.mats.end(), m, m + 10);
+    };
+    push_mat(1.0f, 0.0f, 1.0f, 0.0f, 0.0f, 0.0f, 0.0f, 1.0f);
+    for (const MtlMat& m : mtl) {
+        float rough = std::max(1.0e-2f, m.pr);
+        float metal = m.pm;
+        if (m.illum == 0) {
+            rough = 1.0f;
+            metal = 0.0f;
+        }
+        push_mat(m.ke[0], m.ke[1], m.ke[2], m.kd[0], m.kd[1], m.kd[2], metal, rough);
+    }
+    return 0;
+}
+
+// ==================================================================== octree
+namespace {
+
+const float S3 = std::sqrt(3.0f) / 3;
+const float PN[7][3] = {{1, 0, 0},   {0, 1, 0},    {0, 0, 1},   {S3, S3, S3},
+                        {-S3, S3, S3}, {-S3, -S3, S3}, {S3, -S3, S3}};  // bvh.cpp:8-16
+
+inline float pdot(int i, const float* p) { return PN[i][0] * p[0] + PN[i][1] * p[1] + PN[i][2] * p[2]; }
+inline float fmin_(float a, float b) { return (b < a) ? b : a; }  // std::min
+inline float fmax_(float a, float b) { return (a < b) ? b : a; }  // std::max
+
+struct Builder {
+    const float* T;
+    Octree& t;
+    Builder(const float* tris, Octree& tree) : T(tris), t(tree) {}
+
+    int new_node(const float* mn, const float* mx)
+    {
+        OctNode n;
+        std::memcpy(n.mn, mn, 12);
+        std::memcpy(n.mx, mx, 12);
+        for (int i = 0; i < 7; i++) n.dn[i] = INFINITY, n.df[i] = -INFINITY;
+        for (int i = 0; i < 8; i++) n.child[i] = -1;
+        t.pool.push_back(std::move(n));
+        return (int)t.pool.size() - 1;
+    }
+    void create_children(int ni)  // bvh.h:67-81, including the child _min offsets as written
+    {
+        float mn[3], mx[3];
+        std::memcpy(mn, t.pool[ni].mn, 12);
+        std::memcpy(mx, t.pool[ni].mx, 12);
+        const float cx = (mn[0] + mx[0]) / 2, cy = (mn[1] + mx[1]) / 2, cz = (mn[2] + mx[2]) / 2;
+        const float b[8][6] = {
+            {mn[0], mn[1], mn[2], cx, cy, cz},
+            {cx, mn[1], mn[2], mx[0], cy, cz},
+            {mn[0] + 0.0f, mn[1] + cy, mn[2] + 0.0f, cx, mx[1], cz},
+            {cx, cy, mn[2], mx[0], mx[1], cz},
+            {mn[0] + 0.0f, mn[1] + 0.0f, mn[2] + cz, cx, cy, mx[2]},
+            {cx, mn[1], cz, mx[0], cy, mx[2]},
+            {mn[0] + 0.0f, mn[1] + cy, mn[2] + cz, cx, mx[1], mx[2]},
+            {cx, cy, cz, mx[0], mx[1], mx[2]},
+        };
+        for (int i = 0; i < 8; i++) {
+            int c = new_node(b[i], b[i] + 3);
+            t.pool[ni].child[i] = c;
+        }
+    }
+    void insert(int ni, int id, int depth)  // bvh.h:83-107
+    {
+        const bool exceeded = t.max_depth != -1 && depth == t.max_depth;
+        if (t.pool[ni].leaf || exceeded) {
+            t.pool[ni].tris.push_back(id);
+            if ((int)t.pool[ni].tris.size() > t.leaf_max && !exceeded) {
+                t.pool[ni].leaf = false;
+                create_children(ni);
+                std::vector<int32_t> moved;
+                moved.swap(t.pool[ni].tris);
+                for (int tid : moved) insert_to_children(ni, tid, depth);
+            }
+        } else
+            insert_to_children(ni, id, depth);
+    }
+    void insert_to_children(int ni, int id, int depth)  // bvh.h:109-125
+    {
+        const float* a = T + 9 * (size_t)id;
+        float c[3];
+        for (int k = 0; k < 3; k++) {
+            // Triangle::bbox_centroid (triangle.cpp:3-6): (min + max) * (1.f / 2)
+            float lo = fmin_(a[k], fmin_(a[3 + k], a[6 + k]));
+            float hi = fmax_(a[k], fmax_(a[3 + k], a[6 + k]));
+            c[k] = (1.f / 2) * (lo + hi);
+        }
+        const OctNode& n = t.pool[ni];
+        int o = 0;
+        if (c[0] > (n.mn[0] + n.mx[0]) / 2) o += 1;
+        if (c[1] > (n.mn[1] + n.mx[1]) / 2) o += 2;
+        if (c[2] > (n.mn[2] + n.mx[2]) / 2) o += 4;
+        insert(n.child[o], id, depth + 1);
+    }
+    void compute_volume(int ni)  // bvh.h:55-65 (iterative post-order)
+    {
+        std::vector<std::pair<int, int>> st{{ni, 0}};
+        while (!st.empty()) {
+            auto& [n, k] = st.back();
+            OctNode& nd = t.pool[n];
+            if (nd.leaf) {
+                for (int id : nd.tris) {
+                    const float* a = T + 9 * (size_t)id;
+                    float tn[7], tf[7];
+                    for (int i = 0; i < 7; i++) tn[i] = INFINITY, tf[i] = -INFINITY;
+                    for (int i = 0; i < 7; i++)
+                        for (int j = 0; j < 3; j++) {
+                            float d = pdot(i, a + 3 * j);
+                            tn[i] = fmin_(tn[i], d);
+                            tf[i] = fmax_(tf[i], d);
+                        }
+                    for (int i = 0; i < 7; i++) nd.dn[i] = fmin_(nd.dn[i], tn[i]), nd.df[i] = fmax_(nd.df[i], tf[i]);
+                }
+                st.pop_back();
+                continue;
+            }
+            if (k < 8) {
+                int c = nd.child[k++];
+                st.push_back({c, 0});
+                continue;
+            }
+            for (int i = 0; i < 8; i++) {
+                const OctNode& ch = t.pool[nd.child[i]];
+                for (int p = 0; p < 7; p++) nd.dn[p] = fmin_(nd.dn[p], ch.dn[p]), nd.df[p] = fmax_(nd.df[p], ch.df[p]);
+            }
+            st.pop_back();
+        }
+    }
+};
+
+}  // namespace
+
+void build_octree(const float* tris, int ntris, int max_depth, int leaf_max, Octree& out)
+{
+    out.pool.clear();
+    out.pool.reserve((size_t)ntris / 2 + 16);
+    out.max_depth = max_depth;
+    out.leaf_max = leaf_max;
+    // BVH::BVH (bvh.cpp:19-37): root box from the vertex min / max
+    float mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (int t = 0; t < ntris; t++)
+        for (int j = 0; j < 3; j++)
+            for (int k = 0; k < 3; k++) {
+                float v = tris[9 * (size_t)t + 3 * j + k];
+                mn[k] = fmin_(mn[k], v);
+                mx[k] = fmax_(mx[k], v);
+            }
+    Builder b(tris, out);
+    b.new_node(mn, mx);
+    for (int id = 0; id < ntris; id++) b.insert(0, id, 0);  // bvh.cpp:52-60
+    b.compute_volume(0);
+}
+
+std::vector<char> dump_octree(const Octree& t)
+{
+    std::vector<char> out;
+    auto put = [&](const void* p, size_t n) { out.insert(out.end(), (const char*)p, (const char*)p + n); };
+    std::vector<int> st{0};
+    while (!st.empty()) {
+        int ni = st.back();
+        st.pop_back();
+        const OctNode& n = t.pool[ni];
+        int leaf = n.leaf ? 1 : 0, nt = (int)n.tris.size();
+        put(&leaf, 4);
+        put(&nt, 4);
+        put(n.tris.data(), 4 * n.tris.size());
+        put(n.mn, 12);
+        put(n.mx, 12);
+        put(n.dn, 28);
+        put(n.df, 28);
+        if (!n.leaf)
+            for (int i = 7; i >= 0; i--) st.push_back(n.child[i]);
+    }
+    return out;
+}
+
+int octree_from_dump(const char* buf, size_t bytes, Octree& out)
+{
+    out.pool.clear();
+    size_t o = 0;
+    // stack of (parent, child slot) to attach the next record to
+    std::vector<std::pair<int, int>> st;
+    bool first = true;
+    while (o < bytes) {
+        if (o + 8 > bytes) return -1;
+        int leaf, nt;
+        std::memcpy(&leaf, buf + o, 4);
+        std::memcpy(&nt, buf + o + 4, 4);
+        o += 8;
+        if (nt < 0 || o + 4 * (size_t)nt + 80 > bytes) return -1;
+        OctNode n;
+        n.leaf = leaf != 0;
+        n.tris.resize(nt);
+        std::memcpy(n.tris.data(), buf + o, 4 * (size_t)nt);
+        o += 4 * (size_t)nt;
+        std::memcpy(n.mn, buf + o, 12);
+        std::memcpy(n.mx, buf + o + 12, 12);
+        std::memcpy(n.dn, buf + o + 24, 28);
+        std::memcpy(n.df, buf + o + 52, 28);
+        o += 80;
+        for (int i = 0; i < 8; i++) n.child[i] = -1;
+        out.pool.push_back(std::move(n));
+        const int me = (int)out.pool.size() - 1;
+        if (!first) {
+            if (st.empty()) return -1;
+            auto [par, slot] = st.back();
+            st.pop_back();
+            out.pool[par].child[slot] = me;
+        }
+        first = false;
+        if (!out.pool[me].leaf)
+            for (int i = 7; i >= 0; i--) st.push_back({me, i});
+    }
+    return st.empty() && !first ? 0 : -1;
+}
+
+void flatten_octree(const Octree& t, const float* tris, int ntris, FlatBvh& out)
+{
+    out.nodes.clear();
+    out.tri4.clear();
+    out.prim2k.assign(ntris, -1);
+    out.max_depth = 0;
+    auto empty = [&](int ni) { return t.pool[ni].leaf && t.pool[ni].tris.empty(); };
+    auto fill = [&](RtNode& r, int ni) {
+        std::memcpy(r.dn, t.pool[ni].dn, 28);
+        std::memcpy(r.df, t.pool[ni].df, 28);
+        r.ref = 0;
+        r.cnt = 0;
+    };
+    // Depth-first: a node's children block is allocated when the node is
+    // expanded, so siblings are contiguous and a subtree stays close in memory.
+    struct Item {
+        int ni, rec, depth;
+    };
+    out.nodes.push_back(RtNode{});
+    fill(out.nodes[0], 0);
+    std::vector<Item> st{{0, 0, 0}};
+    while (!st.empty()) {
+        Item it = st.back();
+        st.pop_back();
+        const OctNode& n = t.pool[it.ni];
+        if (!empty(it.ni)) out.max_depth = std::max(out.max_depth, it.depth);
+        if (n.leaf) {
+            out.nodes[it.rec].ref = (uint32_t)(out.tri4.size() / 3);
+            out.nodes[it.rec].cnt = RT_LEAF_BIT | (uint32_t)n.tris.size();
+            for (int id : n.tris) {
+                const float* a = tris + 9 * (size_t)id;
+                float4_ r0{a[0], a[1], a[2], 0.0f}, r1{a[3] - a[0], a[4] - a[1], a[5] - a[2], 0.0f},
+                    r2{a[6] - a[0], a[7] - a[1], a[8] - a[2], 0.0f};
+                std::memcpy(&r0.w, &id, 4);
+                out.prim2k[id] = (int)(out.tri4.size() / 3);
+                out.tri4.push_back(r0);
+                out.tri4.push_back(r1);
+                out.tri4.push_back(r2);
+            }
+            continue;
+        }
+        int kids[8], nk = 0;
+        for (int i = 0; i < 8; i++)
+            if (!empty(n.child[i])) kids[nk++] = n.child[i];
+        const int base = (int)out.nodes.size();
+        out.nodes[it.rec].ref = (uint32_t)base;
+        out.nodes[it.rec].cnt = (uint32_t)nk;
+        out.nodes.resize(base + nk);
+        for (int k = 0; k < nk; k++) fill(out.nodes[base + k], kids[k]);
+        for (int k = nk - 1; k >= 0; k--) st.push_back({kids[k], base + k, it.depth + 1});
+    }
+}
+
+// ======================================================================= env
+void env_luminance_cdf(const float* pix, int w, int h, int channels, float* lum, float* cdf)
+{
+    const size_t n = (size_t)w * h;
+    for (size_t i = 0; i < n; i++) {
+        const float* c = pix + channels * i;
+        lum[i] = 0.3086 * c[0] + 0.6094 * c[1] + 0.0820 * c[2];  // image.h:80-85
+    }
+    if (n == 0) return;
+    cdf[0] = 0.0f;
+    for (size_t i = 0; i < n; i++) cdf[i] = cdf[i > 0 ? i - 1 : 0] + lum[i];  // utils.cpp:126-142
+}
+
+// ==================================================================== camera
+namespace {
+struct Xf {
+    float m[4][4];
+};
+Xf xf_rows(float a00, float a01, float a02, float a03, float a10, float a11, float a12, float a13, float a20, float a21,
+           float a22, float a23, float a30, float a31, float a32, float a33)
+{
+    return Xf{{{a00, a01, a02, a03}, {a10, a11, a12, a13}, {a20, a21, a22, a23}, {a30, a31, a32, a33}}};
+}
+Xf compose(const Xf& a, const Xf& b)  // mat.cpp:364-372
+{
+    Xf m;
+    for (int i = 0; i < 4; i++)
+        for (int j = 0; j < 4; j++)
+            m.m[i][j] = a.m[i][0] * b.m[0][j] + a.m[i][1] * b.m[1][j] + a.m[i][2] * b.m[2][j] + a.m[i][3] * b.m[3][j];
+    return m;
+}
+float radians_(float deg) { return ((float)M_PI / 180.f) * deg; }  // mat.cpp:10-13
+Xf rotation_x(float a)                                             // mat.cpp:210-220
+{
+    volatile float r = radians_(a);  // runtime libm call, as the reference makes it
+    float s = sinf(r), c = cosf(r);
+    return xf_rows(1, 0, 0, 0, 0, c, -s, 0, 0, s, c, 0, 0, 0, 0, 1);
+}
+Xf translation(float x, float y, float z) { return xf_rows(1, 0, 0, x, 0, 1, 0, y, 0, 0, 1, z, 0, 0, 0, 1); }
+const Xf DEFAULT_CS = xf_rows(1, 0, 0, 0, 0, 1, 0, 0, 0, 0, -1, 0, 0, 0, 0, 1);  // camera.cpp:3
+}  // namespace
+
+int camera_preset(const std::string& name, float view[16], float* fov_dist)
+{
+    Xf v;
+    float fov_rad;
+    const float fov = 45;
+    if (name == "default") {  // Camera() (camera.h:18-23)
+        v = DEFAULT_CS;
+        fov_rad = fov / 180.0f * (float)M_PI;
+    } else {
+        Xf t;
+        if (name == "cornell")
+            t = translation(0, 1, 3.5);
+        else if (name == "ganesha")
+            t = compose(rotation_x(-15), translation(-0.0205, 0.67, 1));
+        else if (name == "ite")
+            t = compose(rotation_x(-45), translation(0, 0.15, 1.5));
+        else if (name == "dragon")
+            t = compose(rotation_x(-45), translation(0, -1, 10.5));
+        else if (name == "mis")
+            t = compose(rotation_x(-10), translation(0, -3, 10.5));
+        else
+            return -1;
+        v = compose(t, DEFAULT_CS);  // Camera(float, Transform) (camera.h:30-36)
+        fov_rad = fov / 180.0f * M_PI;
+    }
+    volatile float half = fov_rad / 2.0f;
+    *fov_dist = 1.0f / std::tan((float)half);
+    std::memcpy(view, v.m, 64);
+    return 0;
+}
+
+}  // namespace rt

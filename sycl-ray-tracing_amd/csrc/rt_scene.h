@@ -1,0 +1,73 @@
+// rt_scene.h — host-side scene preparation for the HIP render kernel.
+//
+// Everything here reproduces, bit for bit, the host prerequisites the
+// reference render kernel consumes:
+//   * OBJ/MTL ingest           -> source/utils.cpp:16-98 (+ rapidobj 1.0.1
+//                                 quad split rule, rapidobj.hpp:7164-7225)
+//   * octree BVH build         -> include/bvh.h:55-125, source/bvh.cpp:19-60
+//   * env luminance + CDF      -> include/image.h:80-85, source/utils.cpp:126-142
+//   * camera presets           -> include/camera.h:10-40, source/camera.cpp:3-8
+// and adds the GPU flattening (layout described in DESIGN.md §3).
+#pragma once
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "rt_device.h"
+
+namespace rt {
+
+struct Mesh {
+    std::vector<float> tris;      // [N][9]  Triangle{m_a, m_b, m_c}
+    std::vector<int> mat_idx;     // [N]     material id + 1 (0 = default)
+    std::vector<float> mats;      // [M][10] emission rgba, diffuse rgba, metalness, roughness
+    std::vector<int> emissive;    // emissive triangle ids
+    int ntris() const { return (int)(tris.size() / 9); }
+};
+
+// Parses an OBJ (+ its mtllib) like Utils::parse_obj. Returns 0 or a negative
+// error; `err` receives a message.
+int load_obj(const std::string& path, Mesh& out, std::string& err);
+
+// ---------------------------------------------------------------- octree
+struct OctNode {
+    float mn[3], mx[3];
+    float dn[7], df[7];
+    int32_t child[8];             // pool indices (internal nodes)
+    std::vector<int32_t> tris;    // leaf triangle ids, insertion order
+    bool leaf = true;
+};
+
+struct Octree {
+    std::vector<OctNode> pool;    // pool[0] = root
+    int max_depth = 32, leaf_max = 8;
+};
+
+void build_octree(const float* tris, int ntris, int max_depth, int leaf_max, Octree& out);
+// Pre-order dump identical to oracle/ref/ref_driver.cpp "bvh".
+std::vector<char> dump_octree(const Octree& t);
+// Inverse of dump_octree: rebuilds an Octree from a caller's pre-order walk
+// of BVH::_root (the drop-in path for a reference-built BVH). 0 or <0.
+int octree_from_dump(const char* buf, size_t bytes, Octree& out);
+
+// GPU layout (see rt_device.h for the record formats).
+struct FlatBvh {
+    std::vector<RtNode> nodes;    // nodes[0] = root record
+    std::vector<float4_> tri4;    // 3 records per triangle, leaf order
+    std::vector<int32_t> prim2k;  // triangle id -> leaf-order index
+    int max_depth = 0;            // deepest non-empty node
+};
+void flatten_octree(const Octree& t, const float* tris, int ntris, FlatBvh& out);
+
+// ------------------------------------------------------------------ env
+// lum[i] = (float)(0.3086*r + 0.6094*g + 0.0820*b) in double (image.h:80-85)
+// cdf[i] = cdf[max(i-1,0)] + lum[i] in float, sequential (utils.cpp:126-142)
+void env_luminance_cdf(const float* pix, int w, int h, int channels, float* lum, float* cdf);
+
+// --------------------------------------------------------------- camera
+// Fills view[16] (row-major) and fov_dist for a Camera preset name:
+// default | cornell | ganesha | ite | dragon | mis. Returns 0 or -1.
+int camera_preset(const std::string& name, float view[16], float* fov_dist);
+
+}  // namespace rt

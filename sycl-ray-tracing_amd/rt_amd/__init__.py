@@ -1,0 +1,253 @@
+"""rt_amd — Python mirror of the reference host API over librt_hip.so.
+
+Names, argument meaning and mutation semantics follow the reference
+(TomClabault/SYCL-ray-tracing @ 2024-08-07) so tests read like its own:
+
+  Camera / presets     include/camera.h:10-40, source/camera.cpp:3-8
+  Image                include/image.h:25-178  (RGBA float32, black = (0,0,0,1))
+  parse_obj            source/utils.cpp:16-98  -> ParsedOBJ (include/parsed_obj.h)
+  compute_env_map_cdf  source/utils.cpp:126-142
+  BVH                  include/bvh.h:211-280, source/bvh.cpp:19-37
+  RenderKernel         include/render_kernel.h:21-96
+     render()            mutates the image buffer in place (render_kernel.cpp:189-211)
+     ray_trace_pixel()   one pixel (render_kernel.cpp:75-181)
+
+All compute runs in the native library (C++ host preparation + gfx950 HIP
+kernels); this module only moves numpy buffers across the C ABI.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from ._capi import RtError, check, lib, ptr
+
+__all__ = ["Camera", "Image", "ParsedOBJ", "parse_obj", "compute_env_map_cdf", "luminance_of_pixels", "BVH",
+           "RenderKernel", "RtError", "octree_dump", "make_materials"]
+
+
+# ------------------------------------------------------------------ camera
+class Camera:
+    """view_matrix: 4x4 float32 row-major (Transform::m); fov_dist (camera.h:38-40)."""
+
+    PRESETS = ("default", "cornell", "ganesha", "ite", "dragon", "mis")
+
+    def __init__(self, view_matrix=None, fov_dist=None):
+        if view_matrix is None:
+            c = Camera.preset("default")
+            view_matrix, fov_dist = c.view_matrix, c.fov_dist
+        self.view_matrix = np.ascontiguousarray(view_matrix, dtype=np.float32).reshape(4, 4)
+        self.fov_dist = float(np.float32(fov_dist))
+
+    @staticmethod
+    def preset(name: str) -> "Camera":
+        v = np.zeros(16, dtype=np.float32)
+        f = ctypes.c_float()
+        check(lib(), lib().rt_camera_preset(name.encode(), ptr(v), ctypes.byref(f)), None, f"camera preset {name}")
+        return Camera(v, f.value)
+
+    def as17(self) -> np.ndarray:
+        return np.concatenate([self.view_matrix.ravel(), [np.float32(self.fov_dist)]]).astype(np.float32)
+
+
+# ------------------------------------------------------------------- image
+class Image:
+    """Image(w, h[, color]) — pixels is a [h, w, 4] float32 array (RGBA)."""
+
+    def __init__(self, width: int, height: int, color=(0.0, 0.0, 0.0, 1.0), pixels=None):
+        if pixels is not None:
+            self.pixels = np.ascontiguousarray(pixels, dtype=np.float32).reshape(height, width, 4)
+        else:
+            self.pixels = np.empty((height, width, 4), dtype=np.float32)
+            self.pixels[...] = np.asarray(color, dtype=np.float32)
+        self.width, self.height = width, height
+
+    @staticmethod
+    def from_rgb(rgb: np.ndarray, alpha: float = 0.0) -> "Image":
+        """Like Utils::read_image_float (utils.cpp:100-124): alpha forced to 0."""
+        h, w = rgb.shape[:2]
+        px = np.empty((h, w, 4), dtype=np.float32)
+        px[..., :3] = rgb[..., :3]
+        px[..., 3] = alpha
+        return Image(w, h, pixels=px)
+
+    def data(self) -> np.ndarray:
+        return self.pixels
+
+
+def luminance_of_pixels(img: Image) -> np.ndarray:
+    lum = np.empty(img.width * img.height, dtype=np.float32)
+    cdf = np.empty_like(lum)
+    check(lib(), lib().rt_env_luminance_cdf(ptr(img.pixels), img.width, img.height, 4, ptr(lum), ptr(cdf)))
+    return lum
+
+
+def compute_env_map_cdf(img: Image) -> np.ndarray:
+    lum = np.empty(img.width * img.height, dtype=np.float32)
+    cdf = np.empty_like(lum)
+    check(lib(), lib().rt_env_luminance_cdf(ptr(img.pixels), img.width, img.height, 4, ptr(lum), ptr(cdf)))
+    return cdf
+
+
+# --------------------------------------------------------------------- OBJ
+@dataclass
+class ParsedOBJ:
+    triangles: np.ndarray                  # [N, 9] float32
+    materials: np.ndarray                  # [M, 10] float32
+    emissive_triangle_indices: np.ndarray  # [E] int32
+    material_indices: np.ndarray           # [N] int32
+    spheres: np.ndarray = field(default_factory=lambda: np.zeros((0, 5), np.float32))
+
+
+def parse_obj(path: str) -> ParsedOBJ:
+    L_ = lib()
+    m = ctypes.c_void_p()
+    check(L_, L_.rt_mesh_load(path.encode(), ctypes.byref(m)), None, f"parse_obj({path})")
+    try:
+        nt, nm, ne = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        L_.rt_mesh_counts(m, ctypes.byref(nt), ctypes.byref(nm), ctypes.byref(ne))
+        tris = np.empty((nt.value, 9), np.float32)
+        mi = np.empty(nt.value, np.int32)
+        mats = np.empty((nm.value, 10), np.float32)
+        em = np.empty(ne.value, np.int32)
+        L_.rt_mesh_copy(m, ptr(tris), ptr(mi), ptr(mats), ptr(em))
+    finally:
+        L_.rt_mesh_free(m)
+    return ParsedOBJ(tris, mats, em, mi)
+
+
+def make_materials(rows) -> np.ndarray:
+    """rows of (emission rgb, diffuse rgb, metalness, roughness) -> [M,10] SimpleMaterial buffer."""
+    out = []
+    for e, d, metal, rough in rows:
+        out.append([*e, 1.0, *d, 1.0, metal, rough])
+    return np.asarray(out, dtype=np.float32)
+
+
+def octree_dump(triangles: np.ndarray, max_depth: int = 32, leaf_max: int = 8) -> bytes:
+    tris = np.ascontiguousarray(triangles, dtype=np.float32).reshape(-1, 9)
+    L_ = lib()
+    n = L_.rt_octree_dump(ptr(tris), tris.shape[0], max_depth, leaf_max, None, 0)
+    buf = ctypes.create_string_buffer(n)
+    L_.rt_octree_dump(ptr(tris), tris.shape[0], max_depth, leaf_max, buf, n)
+    return buf.raw
+
+
+class BVH:
+    """BVH(triangles, max_depth=32, leaf_max_obj_count=8) (bvh.cpp:19-37).
+
+    The octree itself is built natively when a RenderKernel binds it. Pass
+    ``preorder=`` (a pre-order walk of a reference BVH::_root) to bind an
+    externally built tree instead."""
+
+    def __init__(self, triangles, max_depth: int = 32, leaf_max_obj_count: int = 8, preorder: bytes | None = None):
+        self.triangles = triangles
+        self.max_depth = max_depth
+        self.leaf_max_obj_count = leaf_max_obj_count
+        self.preorder = preorder
+
+
+# -------------------------------------------------------------- RenderKernel
+class RenderKernel:
+    """RenderKernel(width, height, render_samples, max_bounces, image_buffer,
+    triangles, materials, emissive_triangle_indices, materials_indices,
+    analytic_spheres, bvh, skysphere, env_map_cdf) — render_kernel.h:24-46."""
+
+    def __init__(self, width, height, render_samples, max_bounces, image_buffer: Image, triangle_buffer,
+                 materials_buffer, emissive_triangle_indices_buffer, materials_indices_buffer, analytic_spheres_buffer,
+                 bvh: BVH, skysphere: Image, env_map_cdf, device: int = 0, hostsim: bool = False):
+        self.L = lib(hostsim)
+        self.width, self.height = int(width), int(height)
+        self.render_samples, self.max_bounces = int(render_samples), int(max_bounces)
+        self.frame_buffer = image_buffer
+        h = ctypes.c_void_p()
+        check(self.L, self.L.rt_create(device, ctypes.byref(h)), None, "rt_create")
+        self.ctx = h
+        tris = np.ascontiguousarray(triangle_buffer, dtype=np.float32).reshape(-1, 9)
+        mats = np.ascontiguousarray(materials_buffer, dtype=np.float32).reshape(-1, 10)
+        em = np.ascontiguousarray(emissive_triangle_indices_buffer, dtype=np.int32)
+        mi = np.ascontiguousarray(materials_indices_buffer, dtype=np.int32)
+        sph = np.ascontiguousarray(analytic_spheres_buffer if analytic_spheres_buffer is not None else np.zeros((0, 5)),
+                                   dtype=np.float32).reshape(-1, 5)
+        check(self.L, self.L.rt_set_scene(self.ctx, ptr(tris), tris.shape[0], ptr(mi), mi.shape[0], ptr(mats),
+                                          mats.shape[0], ptr(em), em.shape[0], ptr(sph), sph.shape[0]), self.ctx,
+              "rt_set_scene")
+        if bvh.preorder is not None:
+            buf = ctypes.create_string_buffer(bvh.preorder, len(bvh.preorder))
+            check(self.L, self.L.rt_set_bvh_preorder(self.ctx, buf, len(bvh.preorder)), self.ctx, "rt_set_bvh_preorder")
+        else:
+            check(self.L, self.L.rt_build_bvh(self.ctx, bvh.max_depth, bvh.leaf_max_obj_count), self.ctx,
+                  "rt_build_bvh")
+        cdf = None if env_map_cdf is None else np.ascontiguousarray(env_map_cdf, dtype=np.float32)
+        check(self.L, self.L.rt_set_env(self.ctx, ptr(skysphere.pixels), skysphere.width, skysphere.height, 4,
+                                        ptr(cdf)), self.ctx, "rt_set_env")
+        self.set_camera(Camera())
+
+    def __del__(self):
+        if getattr(self, "ctx", None):
+            self.L.rt_destroy(self.ctx)
+            self.ctx = None
+
+    def set_camera(self, camera: Camera):
+        self.camera = camera
+        check(self.L, self.L.rt_set_camera(self.ctx, ptr(camera.view_matrix), camera.fov_dist), self.ctx,
+              "rt_set_camera")
+
+    def render(self):
+        fb = self.frame_buffer.pixels
+        assert fb.flags.c_contiguous and fb.dtype == np.float32 and fb.shape == (self.height, self.width, 4)
+        check(self.L, self.L.rt_render(self.ctx, self.width, self.height, self.render_samples, self.max_bounces,
+                                       ptr(fb)), self.ctx, "rt_render")
+
+    def render_device(self, d_fb: int, row_offset: int = 0, row_stride: int = 1, stream: int | None = None):
+        """Render into a device buffer (e.g. a torch tensor's data_ptr()); no host copies."""
+        check(self.L, self.L.rt_render_device(self.ctx, self.width, self.height, self.render_samples,
+                                              self.max_bounces, ctypes.c_void_p(d_fb), row_offset, row_stride,
+                                              ctypes.c_void_p(stream) if stream else None), self.ctx,
+              "rt_render_device")
+
+    def ray_trace_pixels(self, xy) -> None:
+        xy = np.ascontiguousarray(xy, dtype=np.int32).reshape(-1, 2)
+        fb = self.frame_buffer.pixels
+        rgba = np.ascontiguousarray(fb[xy[:, 1], xy[:, 0]])
+        check(self.L, self.L.rt_render_pixels(self.ctx, self.width, self.height, self.render_samples,
+                                              self.max_bounces, ptr(xy), xy.shape[0], ptr(rgba)), self.ctx,
+              "rt_render_pixels")
+        fb[xy[:, 1], xy[:, 0]] = rgba
+
+    def ray_trace_pixel(self, x: int, y: int) -> None:
+        self.ray_trace_pixels(np.array([[x, y]], dtype=np.int32))
+
+    def intersect(self, rays) -> np.ndarray:
+        rays = np.ascontiguousarray(rays, dtype=np.float32).reshape(-1, 6)
+        out = np.zeros((rays.shape[0], 11), dtype=np.int32)
+        check(self.L, self.L.rt_intersect(self.ctx, ptr(rays), rays.shape[0], ptr(out)), self.ctx, "rt_intersect")
+        return out
+
+    def set_stats(self, on: bool):
+        self.L.rt_set_stats(self.ctx, 1 if on else 0)
+
+    def stats(self) -> np.ndarray:
+        out = np.zeros(8, dtype=np.uint64)
+        self.L.rt_get_stats(self.ctx, ptr(out), 8)
+        return out
+
+    def last_kernel_ms(self) -> float:
+        return float(self.L.rt_last_kernel_ms(self.ctx))
+
+    def device_last_kernel_ms(self) -> float:
+        return float(self.L.rt_device_last_kernel_ms(self.ctx))
+
+    def bvh_info(self) -> dict:
+        info = np.zeros(5, dtype=np.int64)
+        check(self.L, self.L.rt_bvh_info(self.ctx, ptr(info)), self.ctx, "rt_bvh_info")
+        return dict(octree_nodes=int(info[0]), gpu_records=int(info[1]), triangles=int(info[2]),
+                    max_depth=int(info[3]), gpu_bytes=int(info[4]))
+
+    def bvh_dump(self) -> bytes:
+        n = self.L.rt_bvh_dump(self.ctx, None, 0)
+        buf = ctypes.create_string_buffer(n)
+        self.L.rt_bvh_dump(self.ctx, buf, n)
+        return buf.raw
