@@ -1,0 +1,220 @@
+"""bench.py — render throughput of the MI355X path tracer (BASELINE.json metric).
+
+A "step" is one full render of the configured frame (RenderKernel::render,
+render_kernel.cpp:189-211): every pixel, every sample, every bounce, then the
+in-place tone-map, plus (N > 1) the RCCL gather of the HDR shards to rank 0.
+Scene, BVH, env map and camera are resident in HBM before timing starts
+(the reference times render() only, main.cpp:93-116).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config cfg2]
+  N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+
+Rank 0 prints ONE JSON line. Extra objects:
+  roofline      the render kernel's algorithmic bytes per launch (SURVEY.md
+                §8(d) byte model x the kernel's own traversal counters, read
+                from a stats-enabled render of the same workload) / its mean
+                launch time from HIP events on the launch stream, vs 8 TB/s.
+                `traffic` is the PMC-measured HBM bytes per launch from
+                profiles/ (rocprofv3 --pmc pass of this command), or null.
+  cpu_baseline  the pinned CPU restatement oracle (oracle/cpu_oracle.cpp,
+                "port") on a bounded row subset of the same frame, on the
+                host cores; its rows are also compared with the GPU's
+                (parity, per-channel L-inf after tone-map).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+for p in (os.path.join(REPO, "sycl-ray-tracing_amd"), os.path.join(REPO, "tools"), os.path.join(REPO, "tests")):
+    sys.path.insert(0, p)
+
+import numpy as np  # noqa: E402
+
+CONFIGS = {
+    # name: (scene, sky, camera, W, H, spp, bounces, description)
+    "cfg1": ("cornell12", "S", "cornell", 256, 256, 4, 3, "Cornell 12-tri 256x256x4spp x3"),
+    "cfg2": ("dragon", "L", "dragon", 1920, 1080, 64, 8,
+             "PBRT Dragon stand-in (1,000,002 tris) 1920x1080x64spp x8 bounces, SKY-L 2048x1024 env IS+MIS"),
+    "cfg3": ("dragon", "L", "dragon", 1920, 1080, 256, 8,
+             "PBRT Dragon stand-in 1920x1080x256spp x8 bounces, SKY-L env IS+MIS"),
+    "cfg4": ("dragon", "L", "dragon", 3840, 2160, 256, 8, "PBRT Dragon stand-in 3840x2160x256spp x8 bounces"),
+}
+HBM_PEAK_GBS = 8000.0  # /opt/skills/guides/MI355X_MICROARCH.md (spec)
+# SURVEY.md §8(d) byte model: per child-volume test 56 B (7+7 f32 planes),
+# per triangle test 36 B (3 vertices), per material fetch 40 B, per env
+# texel 16 B, per CDF probe 4 B.
+BYTES = {"vol": 56, "tri": 36, "mat": 40, "env": 16, "cdf": 4}
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def build_inputs(cfg):
+    import rt_amd
+    import scenes
+    scene, sky_kind, cam, W, H, spp, nb, _ = CONFIGS[cfg]
+    P = rt_amd.parse_obj(scenes.scene_path(scene))
+    sky = scenes.make_sky(sky_kind)
+    cam17 = rt_amd.Camera.preset(cam).as17()
+    return P, sky, cam17
+
+
+def cpu_baseline(P, sky, cam17, cfg, gpu_frame, threads, row_step):
+    """Oracle on every row_step-th row (full spp) of the same frame."""
+    from oracle_bindings import OracleScene
+    import golden_io as gio
+    _, _, _, W, H, spp, nb, _ = CONFIGS[cfg]
+    S = OracleScene(P.triangles, P.material_indices, P.materials, P.emissive_triangle_indices, env=sky)
+    rows = np.arange(row_step // 2, H, row_step)
+    xs, ys = np.meshgrid(np.arange(W), rows)
+    px = np.stack([xs.ravel(), ys.ravel()], 1).astype(np.int32)
+    res, sec = S.render(cam17, W, H, spp, nb, pixels=px, threads=threads)
+    samples = px.shape[0] * spp
+    par = gio.compare_rgb(gpu_frame[rows].reshape(-1, 4), res) if gpu_frame is not None else None
+    return dict(value=samples / sec / 1e6, unit="Msamples/s", cores=threads, kind="port",
+                sample=f"{rows.size} rows (every {row_step}th row, all {W} px, {spp} spp, {nb} bounces) = "
+                       f"{samples / 1e6:.2f} Msamples in {sec:.2f} s, OpenMP dynamic over pixels"), par
+
+
+def load_traffic(cfg, n_gpus):
+    """PMC HBM bytes per launch from a committed rocprofv3 --pmc pass."""
+    p = os.path.join(REPO, "profiles", "traffic.json")
+    if not os.path.exists(p):
+        return None
+    d = json.load(open(p))
+    e = d.get(f"{cfg}_n{n_gpus}") or d.get(cfg)
+    return None if e is None else e.get("bytes_per_launch")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--config", default="cfg2", choices=sorted(CONFIGS))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-stats", action="store_true", help="skip the counter pass (roofline.achieved = null)")
+    ap.add_argument("--cpu-row-step", type=int, default=10)
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    rank = int(os.environ.get("RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    local = int(os.environ.get("LOCAL_RANK", 0))
+    if world != args.gpus:
+        log(f"note: WORLD_SIZE={world} but --gpus={args.gpus}; using WORLD_SIZE")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    import rt_amd
+    from rt_amd.dist import ShardedFrame
+    scene, sky_kind, cam, W, H, spp, nb, desc = CONFIGS[args.config]
+
+    t0 = time.time()
+    if rank == 0:
+        build_inputs(args.config)  # materialise the scene file once
+    if world > 1:
+        dist.barrier()
+    P, sky, cam17 = build_inputs(args.config)
+    rk = rt_amd.RenderKernel(W, H, spp, nb, rt_amd.Image(1, 1), P.triangles, P.materials,
+                             P.emissive_triangle_indices, P.material_indices, None, rt_amd.BVH(P.triangles),
+                             rt_amd.Image.from_rgb(sky), None, device=local)
+    rk.set_camera(rt_amd.Camera(cam17[:16], cam17[16]))
+    frame = ShardedFrame(rk, rank, world, device=dev)
+    info = rk.bvh_info()
+    log(f"[rank {rank}] setup {time.time() - t0:.1f}s  bvh {info}")
+
+    stream = torch.cuda.current_stream(dev).cuda_stream
+
+    # counter pass (same workload, stats kernel variant) -> algorithmic bytes
+    stats = None
+    if not args.no_stats:
+        rk.set_stats(True)
+        frame.render(stream)
+        torch.cuda.synchronize(dev)
+        s = rk.stats().astype(np.float64)
+        rk.set_stats(False)
+        stats = dict(rays=s[0], vol=s[1], tri=s[2], leaf=s[3], mat=s[4], env=s[5], cdf=s[6], heap_slow=s[7])
+        log(f"[rank {rank}] counters {stats}")
+
+    for _ in range(args.warmup):
+        frame.render(stream)
+        frame.gather()
+    torch.cuda.synchronize(dev)
+
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    kms = []
+    t_start = time.perf_counter()
+    for _ in range(args.steps):
+        frame.render(stream)
+        full = frame.gather()
+        torch.cuda.synchronize(dev)
+        kms.append(rk.device_last_kernel_ms())
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t_start
+
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+    kernel_ms = float(np.mean(kms))
+
+    samples_per_step = W * H * spp
+    value = samples_per_step * args.steps / elapsed / 1e6
+
+    roofline = None
+    if stats is not None:
+        algo = (BYTES["vol"] * stats["vol"] + BYTES["tri"] * stats["tri"] + BYTES["mat"] * stats["mat"] +
+                BYTES["env"] * stats["env"] + BYTES["cdf"] * stats["cdf"])
+        achieved = algo / (kernel_ms * 1e-3) / 1e9
+        roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": load_traffic(args.config, world),
+                    "algo_bytes_per_launch": algo, "bytes_per_sample": round(algo / (frame.rows * W * spp), 1),
+                    "rays_per_sample": round(stats["rays"] / (frame.rows * W * spp), 3),
+                    "kernel_ms": round(kernel_ms, 3)}
+
+    cpu = None
+    parity = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        threads = int(os.environ.get("OMP_NUM_THREADS", 0)) or len(os.sched_getaffinity(0))
+        threads = min(threads, len(os.sched_getaffinity(0)))
+        gpu_frame = full.cpu().numpy()
+        cpu, parity = cpu_baseline(P, sky, cam17, args.config, gpu_frame, threads, args.cpu_row_step)
+
+    if world > 1:
+        dist.barrier()
+    if rank == 0:
+        out = {
+            "metric": "Msamples/sec (W×H×spp/s) at 1080p; per-channel L∞ vs CPU ref",
+            "value": round(value, 3), "unit": "Msamples/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic: procedural 1,000,002-triangle stand-in for the absent pbrt_dragon.obj and a "
+                    "synthetic 2048x1024 env map (SURVEY.md §8d)",
+            "config": {"workload": f"{args.config}: {desc}", "W": W, "H": H, "spp": spp, "bounces": nb,
+                       "parallelism": f"rows y%{world} per GPU + RCCL gather" if world > 1 else "1 GPU"},
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+            "parity": parity,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -717,7 +717,9 @@ void* oracle_scene_create(const float* tris, int ntri, const int* mat_idx, const
     Scene* S = new Scene();
     S->tris.resize(ntri);
     std::memcpy(S->tris.data(), tris, sizeof(float) * 9 * (size_t)ntri);
-    S->mat_idx.assign(mat_idx, mat_idx + ntri);
+    // one material index per triangle, then one per sphere (main.cpp:20-30
+    // add_sphere_to_scene appends them in that order)
+    S->mat_idx.assign(mat_idx, mat_idx + ntri + nsph);
     S->mats.resize(nmat);
     for (int i = 0; i < nmat; i++) {
         const float* p = mats + 10 * i;  // emission rgba, diffuse rgba, metalness, roughness

@@ -28,22 +28,28 @@ static void merge_stats(rt_context* c, const std::vector<rtk::Stats>& s)
 int rt_backend_render(rt_context* c, int w, int h, int spp, int bounces, float* host_fb, void* dev_fb, int row_offset,
                       int row_stride, void*)
 {
-    if (!host_fb) return rt_fail(c, RT_ERR_NODEV, "hostsim: device buffers are not supported");
-    (void)dev_fb;
+    // host_fb: the full frame (rt_render). dev_fb: in this build a host
+    // pointer to a compacted row shard, row j = image row row_offset +
+    // j*row_stride (rt_render_device semantics, used by the gloo tests).
+    float* out = host_fb ? host_fb : (float*)dev_fb;
+    const bool shard = host_fb == nullptr;
     rtk::Ctx C{rt_host_view(c), c->cam, w, h, spp, bounces};
     std::vector<rtk::Stats> st(omp_get_max_threads());
     for (auto& s : st) std::memset(&s, 0, sizeof s);
+    const int rows_local = (h - row_offset + row_stride - 1) / row_stride;
     const double t0 = omp_get_wtime();
 #pragma omp parallel
     {
         std::vector<rtk::StackEnt> stack(RT_STACK_CAP);
         rtk::Stats* ps = c->stats_enabled ? &st[omp_get_thread_num()] : nullptr;
 #pragma omp for schedule(dynamic)
-        for (int y = row_offset; y < h; y += row_stride)
+        for (int j = 0; j < rows_local; j++) {
+            const int y = row_offset + j * row_stride;
             for (int x = 0; x < w; x++) {
                 rtk::Col f = rtk::trace_pixel(C, x, y, stack.data(), ps);
-                rtk::tonemap_into(host_fb + 4 * ((size_t)y * w + x), f);
+                rtk::tonemap_into(out + 4 * ((size_t)(shard ? j : y) * w + x), f);
             }
+        }
     }
     c->last_kernel_ms = (omp_get_wtime() - t0) * 1e3;
     merge_stats(c, st);

@@ -58,6 +58,7 @@ class OracleScene:
         self.spheres = np.ascontiguousarray(spheres if spheres is not None else np.zeros((0, 5)), dtype=np.float32)
         self.env = None if env is None else np.ascontiguousarray(env, dtype=np.float32)
         eh, ew = (0, 0) if env is None else self.env.shape[:2]
+        assert self.mat_idx.shape[0] >= self.tris.shape[0] + self.spheres.shape[0], "one material index per primitive"
         self.h = lib().oracle_scene_create(
             _p(self.tris), self.tris.shape[0], _p(self.mat_idx), _p(self.mats), self.mats.shape[0],
             _p(self.emissive), self.emissive.shape[0], _p(self.spheres), self.spheres.shape[0],

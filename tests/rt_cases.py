@@ -1,0 +1,83 @@
+"""Render cases shared by the parity tests: the golden fixtures written by
+the compiled reference (tools/gen_golden.py, tests/golden/manifest.json) and
+helpers to run the same case through the product (gfx950), the hostsim build
+of the product's device code, or the CPU restatement oracle."""
+from __future__ import annotations
+
+import numpy as np
+
+import scenes
+from conftest import load_golden, parsed_scene
+
+import rt_amd
+
+_sky = {}
+
+
+def sky(kind: str) -> np.ndarray:
+    if kind not in _sky:
+        _sky[kind] = scenes.make_sky(kind)
+    return _sky[kind]
+
+
+def materials_for(entry: dict, P) -> np.ndarray:
+    mats = P.materials.copy()
+    mo = entry.get("mat_override")
+    if mo:
+        mats[mo["index"], 8] = np.float32(repr(mo["metalness"]))
+        mats[mo["index"], 9] = np.float32(repr(mo["roughness"]))
+    return mats
+
+
+def golden_case(name: str, manifest: dict) -> dict:
+    e = dict(manifest["renders"][name])
+    g = load_golden(f"render_{name}.npz")
+    e["name"] = name
+    e["expected"] = g["rgba"]
+    e["px"] = g.get("px")
+    return e
+
+
+def make_kernel(entry: dict, cameras: dict, hostsim: bool, W=None, H=None, spp=None, bounces=None, fb=None,
+                spheres=None):
+    P = parsed_scene(entry["scene"])
+    W = W or entry["W"]
+    H = H or entry["H"]
+    fb = fb if fb is not None else rt_amd.Image(W, H)
+    c = cameras[entry["camera"]]
+    rk = rt_amd.RenderKernel(W, H, spp or entry["spp"], bounces or entry["bounces"], fb, P.triangles,
+                             materials_for(entry, P), P.emissive_triangle_indices, P.material_indices, spheres,
+                             rt_amd.BVH(P.triangles), rt_amd.Image.from_rgb(sky(entry["sky"])), None,
+                             hostsim=hostsim)
+    rk.set_camera(rt_amd.Camera(c[:16], c[16]))
+    return rk, fb
+
+
+def run_case(entry: dict, cameras: dict, hostsim: bool) -> np.ndarray:
+    """Returns the tone-mapped RGBA of the case (full frame or its pixel list)."""
+    rk, fb = make_kernel(entry, cameras, hostsim)
+    if entry.get("px") is None:
+        rk.render()
+        return fb.pixels
+    rk.ray_trace_pixels(entry["px"])
+    px = entry["px"]
+    return fb.pixels[px[:, 1], px[:, 0]]
+
+
+def oracle_scene(entry: dict):
+    from oracle_bindings import OracleScene
+    P = parsed_scene(entry["scene"])
+    return OracleScene(P.triangles, P.material_indices, materials_for(entry, P), P.emissive_triangle_indices,
+                       env=sky(entry["sky"]))
+
+
+def run_oracle(entry: dict, cameras: dict, threads: int = 0) -> np.ndarray:
+    S = oracle_scene(entry)
+    res, _ = S.render(cameras[entry["camera"]], entry["W"], entry["H"], entry["spp"], entry["bounces"],
+                      pixels=entry.get("px"), threads=threads)
+    return res
+
+
+CORNELL_CASES = ["cfg1_cornell12", "cornell32_128", "cornell32_64spp", "mis_512"]
+DRAGON_CASES = ["cfg2_dragon", "cfg3_dragon", "cfg4_dragon4k"] + [
+    f"cfg5_sweep_m{m}_r{r}" for m in range(4) for r in range(4)]

@@ -1,0 +1,224 @@
+"""GPU parity: the product library librt_hip.so (gfx950 kernel) through the
+C ABI against (1) the golden renders the compiled reference produced and (2)
+the pinned CPU restatement oracle on the same seeded inputs.
+
+Tolerance (BASELINE.json north_star): per-channel L-inf <= 1e-4 on the
+tone-mapped RGB, NaN == NaN. The kernel is built to be bit-exact, so the
+bitwise-identical fraction is also asserted (>= 0.9999)."""
+from __future__ import annotations
+
+import ctypes
+import ctypes.util
+
+import numpy as np
+import pytest
+
+import golden_io as gio
+import rt_cases
+from conftest import load_golden, parsed_scene
+
+import rt_amd
+from rt_amd import _capi
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-4
+
+
+def assert_parity(got, want, min_bitwise=0.9999):
+    c = gio.compare_rgb(got, want)
+    print("parity", c)
+    assert c["nan_mismatch"] == 0, c
+    assert c["linf"] <= TOL, c
+    assert c["pixels_over_1e4"] == 0, c
+    assert c["bitwise_fraction"] >= min_bitwise, c
+
+
+@pytest.mark.parametrize("name", rt_cases.CORNELL_CASES + rt_cases.DRAGON_CASES)
+def test_gpu_matches_reference_goldens(name, manifest, cameras):
+    e = rt_cases.golden_case(name, manifest)
+    got = rt_cases.run_case(e, cameras, hostsim=False)
+    assert_parity(got, e["expected"])
+
+
+def test_gpu_cfg2_full_frame_rows_match_oracle(manifest, cameras):
+    """Cfg2 (dragon, 1920x1080x64spp x8) rendered as a whole frame on the
+    GPU; every 60th row is re-rendered by the oracle and compared."""
+    e = rt_cases.golden_case("cfg2_dragon", manifest)
+    rk, fb = rt_cases.make_kernel(e, cameras, hostsim=False)
+    rk.render()
+    rows = np.arange(7, e["H"], 60)
+    xs, ys = np.meshgrid(np.arange(e["W"]), rows)
+    e["px"] = np.stack([xs.ravel(), ys.ravel()], 1).astype(np.int32)
+    want = rt_cases.run_oracle(e, cameras)
+    assert_parity(fb.pixels[rows].reshape(-1, 4), want)
+    # and the golden pixels
+    g = rt_cases.golden_case("cfg2_dragon", manifest)
+    assert_parity(fb.pixels[g["px"][:, 1], g["px"][:, 0]], g["expected"])
+
+
+def test_gpu_row_shards_bit_identical(manifest, cameras):
+    """rt_render_device row shards == rows of the full frame, bit for bit
+    (the multi-GPU partition)."""
+    import torch
+    e = rt_cases.golden_case("cornell32_128", manifest)
+    for stride in (2, 3, 8):
+        for off in range(stride):
+            rk, _ = rt_cases.make_kernel(e, cameras, hostsim=False)
+            rows = len(range(off, e["H"], stride))
+            shard = torch.zeros((rows, e["W"], 4), dtype=torch.float32, device="cuda")
+            shard[..., 3] = 1.0
+            torch.cuda.synchronize()
+            rk.render_device(shard.data_ptr(), off, stride, torch.cuda.current_stream().cuda_stream)
+            torch.cuda.synchronize()
+            got = shard.cpu().numpy()
+            np.testing.assert_array_equal(got.view(np.uint32), e["expected"][off::stride].view(np.uint32))
+
+
+def test_gpu_reference_bvh_regression_rays():
+    """source/tests.cpp:16-58 / include/bvh_tests.h through the gfx950 traversal."""
+    P = parsed_scene("cornell")
+    sky = rt_amd.Image.from_rgb(rt_cases.sky("S"))
+    rk = rt_amd.RenderKernel(4, 4, 1, 1, rt_amd.Image(4, 4), P.triangles, P.materials, P.emissive_triangle_indices,
+                             P.material_indices, None, rt_amd.BVH(P.triangles), sky, None)
+    g = load_golden("bvhtests_cornell.npz")
+    for part, hits in (("inter", True), ("miss", False)):
+        rec = g[part]
+        out = rk.intersect(np.concatenate([rec["o"], rec["d"]], axis=1))
+        assert (out[:, 0] == int(hits)).all()
+        if hits:
+            assert np.all(np.abs(out[:, 3:6].view(np.float32) - rec["expect"]) <= 1e-5)
+            np.testing.assert_array_equal(out[:, 1], rec["bvh"]["prim"])
+            np.testing.assert_array_equal(out[:, 2].view(np.float32), rec["bvh"]["t"])
+
+
+def test_gpu_dragon_rays_match_reference():
+    P = parsed_scene("dragon")
+    sky = rt_amd.Image.from_rgb(rt_cases.sky("S"))
+    rk = rt_amd.RenderKernel(4, 4, 1, 1, rt_amd.Image(4, 4), P.triangles, P.materials, P.emissive_triangle_indices,
+                             P.material_indices, None, rt_amd.BVH(P.triangles), sky, None)
+    g = load_golden("rays_dragon.npz")
+    out = rk.intersect(g["rays"])
+    h = g["hits"]
+    np.testing.assert_array_equal(out[:, 0], h["found"])
+    hit = h["found"] == 1
+    np.testing.assert_array_equal(out[hit, 1], h["prim"][hit])
+    np.testing.assert_array_equal(out[hit, 2].view(np.float32), h["t"][hit])
+    np.testing.assert_array_equal(out[hit, 3:6].view(np.float32), h["p"][hit])
+    np.testing.assert_array_equal(out[hit, 6:9].view(np.float32), h["n"][hit])
+
+
+def test_gpu_spheres_match_oracle(cameras):
+    from oracle_bindings import OracleScene
+    from test_hostsim import sphere_scene
+    P, mats, mi, sph = sphere_scene()
+    sky = rt_cases.sky("S")
+    S = OracleScene(P.triangles, mi, mats, P.emissive_triangle_indices, env=sky, spheres=sph)
+    want, _ = S.render(cameras["cornell"], 96, 96, 4, 4)
+    fb = rt_amd.Image(96, 96)
+    rk = rt_amd.RenderKernel(96, 96, 4, 4, fb, P.triangles, mats, P.emissive_triangle_indices, mi, sph,
+                             rt_amd.BVH(P.triangles), rt_amd.Image.from_rgb(sky), None)
+    c = cameras["cornell"]
+    rk.set_camera(rt_amd.Camera(c[:16], c[16]))
+    rk.render()
+    assert_parity(fb.pixels, want, min_bitwise=1.0)
+
+
+def test_gpu_random_configs_match_oracle(cameras):
+    """Seeded sweep of small configs (sizes, spp, bounce counts incl. 0/1 and
+    the H<25 case that crashes the reference's progress print) vs the oracle."""
+    from oracle_bindings import OracleScene
+    rng = np.random.default_rng(11)
+    for scene, sky_kind, cam in (("cornell", "S", "cornell"), ("mis", "S", "mis"), ("cornell12", "S", "cornell")):
+        P = parsed_scene(scene)
+        S = OracleScene(P.triangles, P.material_indices, P.materials, P.emissive_triangle_indices,
+                        env=rt_cases.sky(sky_kind))
+        for _ in range(3):
+            W, H = int(rng.integers(1, 90)), int(rng.integers(1, 70))
+            spp, nb = int(rng.integers(1, 9)), int(rng.integers(0, 10))
+            want, _ = S.render(cameras[cam], W, H, spp, nb)
+            fb = rt_amd.Image(W, H)
+            rk = rt_amd.RenderKernel(W, H, spp, nb, fb, P.triangles, P.materials, P.emissive_triangle_indices,
+                                     P.material_indices, None, rt_amd.BVH(P.triangles),
+                                     rt_amd.Image.from_rgb(rt_cases.sky(sky_kind)), None)
+            c = cameras[cam]
+            rk.set_camera(rt_amd.Camera(c[:16], c[16]))
+            rk.render()
+            assert_parity(fb.pixels, want, min_bitwise=1.0)
+
+
+# ------------------------------------------------------------ device libm
+_FN = {0: "expf", 2: "sinf", 3: "cosf", 4: "acosf", 5: "asinf"}
+
+
+def _glibc():
+    m = ctypes.CDLL(ctypes.util.find_library("m"))
+    for n in ("expf", "sinf", "cosf", "acosf", "asinf"):
+        getattr(m, n).restype = ctypes.c_float
+        getattr(m, n).argtypes = [ctypes.c_float]
+    for n in ("powf", "atan2f"):
+        getattr(m, n).restype = ctypes.c_float
+        getattr(m, n).argtypes = [ctypes.c_float, ctypes.c_float]
+    return m
+
+
+def _inputs(fn, rng, n):
+    if fn == 0:
+        x = rng.uniform(-104, 89, n)
+    elif fn in (2, 3):
+        x = np.concatenate([rng.uniform(0, 2 * np.pi, n // 2), rng.uniform(-1e4, 1e4, n - n // 2)])
+    else:
+        x = rng.uniform(-1, 1, n)
+    x = x.astype(np.float32)
+    special = np.array([0.0, -0.0, 1.0, -1.0, np.inf, -np.inf, np.nan, 1e-40, -1e-40, 3.14159265, 1.5707964],
+                       np.float32)
+    return np.concatenate([special, x])
+
+
+@pytest.mark.parametrize("fn", sorted(_FN))
+def test_gpu_libm_unary_matches_glibc(fn):
+    """rt_libm.h on gfx950 == this image's glibc 2.35 float libm, bit for bit."""
+    m = _glibc()
+    f = getattr(m, _FN[fn])
+    x = _inputs(fn, np.random.default_rng(fn), 20000)
+    out = np.zeros_like(x)
+    assert _capi.lib().rt_device_libm(0, fn, _capi.ptr(x), None, _capi.ptr(out), x.shape[0]) == 0
+    want = np.array([f(float(v)) for v in x], np.float32)
+    same = (out.view(np.uint32) == want.view(np.uint32)) | (np.isnan(out) & np.isnan(want))
+    assert same.all(), (x[~same][:5], out[~same][:5], want[~same][:5])
+
+
+@pytest.mark.parametrize("fn", [1, 6])
+def test_gpu_libm_binary_matches_glibc(fn):
+    m = _glibc()
+    rng = np.random.default_rng(100 + fn)
+    n = 20000
+    if fn == 1:  # powf at the exponents the path uses: 5 (fresnel) and 1/2.2 (gamma)
+        x = rng.uniform(0, 1.0, n).astype(np.float32)
+        y = np.where(rng.random(n) < 0.5, np.float32(5.0), np.float32(1.0) / np.float32(2.2)).astype(np.float32)
+        f = m.powf
+    else:
+        x = rng.uniform(-1, 1, n).astype(np.float32)
+        y = rng.uniform(-1, 1, n).astype(np.float32)
+        f = m.atan2f
+    out = np.zeros_like(x)
+    assert _capi.lib().rt_device_libm(0, fn, _capi.ptr(x), _capi.ptr(y), _capi.ptr(out), n) == 0
+    want = np.array([f(float(a), float(b)) for a, b in zip(x, y)], np.float32)
+    same = (out.view(np.uint32) == want.view(np.uint32)) | (np.isnan(out) & np.isnan(want))
+    assert same.all()
+
+
+def test_gpu_ieee_div_sqrt_f64():
+    """IEEE f32 division / sqrt with denormals, and the f64 GGX path, on device."""
+    rng = np.random.default_rng(5)
+    x = np.concatenate([rng.uniform(-10, 10, 5000), rng.uniform(0, 1e-36, 1000)]).astype(np.float32)
+    y = np.concatenate([rng.uniform(-10, 10, 5000), rng.uniform(1, 1e3, 1000)]).astype(np.float32)
+    L = _capi.lib()
+    out = np.zeros_like(x)
+    assert L.rt_device_libm(0, 8, _capi.ptr(x), _capi.ptr(y), _capi.ptr(out), x.shape[0]) == 0
+    np.testing.assert_array_equal(out.view(np.uint32), (x / y).astype(np.float32).view(np.uint32))
+    ax = np.abs(x)
+    assert L.rt_device_libm(0, 7, _capi.ptr(ax), None, _capi.ptr(out), x.shape[0]) == 0
+    np.testing.assert_array_equal(out.view(np.uint32), np.sqrt(ax).view(np.uint32))
+    assert L.rt_device_libm(0, 9, _capi.ptr(x), _capi.ptr(y), _capi.ptr(out), x.shape[0]) == 0
+    want = (x.astype(np.float64) * 0.31830988618379067154 / y.astype(np.float64)).astype(np.float32)
+    np.testing.assert_array_equal(out.view(np.uint32), want.view(np.uint32))

@@ -116,7 +116,7 @@ def write_dragon_standin(path: str, n_theta: int = 500, n_phi: int = 1000) -> st
     f = dragon_faces(n_theta, n_phi) + 1
     nv = v.shape[0]
     ground_v = np.array([[-20.0, 0.0, -20.0], [-20.0, 0.0, 20.0], [20.0, 0.0, 20.0], [20.0, 0.0, -20.0]])
-    tmp = path + ".tmp"
+    tmp = f"{path}.{os.getpid()}.tmp"
     with open(tmp, "w") as fh:
         fh.write("# procedural stand-in for pbrt_dragon.obj (tools/scenes.py)\nmtllib pbrt_dragon.mtl\n")
         fh.write("o dragon_standin\n")
