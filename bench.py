@@ -47,8 +47,17 @@ CONFIGS = {
 HBM_PEAK_GBS = 8000.0  # /opt/skills/guides/MI355X_MICROARCH.md (spec)
 # SURVEY.md §8(d) byte model: per child-volume test 56 B (7+7 f32 planes),
 # per triangle test 36 B (3 vertices), per material fetch 40 B, per env
-# texel 16 B, per CDF probe 4 B.
+# texel 16 B, per CDF probe 4 B. The dominant kernel is the closest-hit
+# trace; its algorithmic bytes are its own volume and triangle tests.
 BYTES = {"vol": 56, "tri": 36, "mat": 40, "env": 16, "cdf": 4}
+
+
+def algo_bytes(st: dict, kernel: str) -> float:
+    if kernel == "trace_closest":
+        return BYTES["vol"] * st["vol"] + BYTES["tri"] * st["tri"]
+    if kernel == "trace_any":
+        return BYTES["vol"] * st["any_vol"] + BYTES["tri"] * st["any_tri"]
+    return BYTES["mat"] * st["mat"] + BYTES["env"] * st["env"] + BYTES["cdf"] * st["cdf"]
 
 
 def log(*a):
@@ -142,10 +151,9 @@ def main():
         rk.set_stats(True)
         frame.render(stream)
         torch.cuda.synchronize(dev)
-        s = rk.stats().astype(np.float64)
+        stats = rk.stats()
         rk.set_stats(False)
-        stats = dict(rays=s[0], vol=s[1], tri=s[2], leaf=s[3], mat=s[4], env=s[5], cdf=s[6], heap_slow=s[7])
-        log(f"[rank {rank}] counters {stats}")
+        log(f"[rank {rank}] counters {stats}  iterations {rk.last_iterations()}")
 
     for _ in range(args.warmup):
         frame.render(stream)
@@ -155,17 +163,19 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
+    rk.kernel_timing(1)  # HIP events around every kernel launch, on the launch stream
     kms = []
     t_start = time.perf_counter()
     for _ in range(args.steps):
         frame.render(stream)
         full = frame.gather()
-        torch.cuda.synchronize(dev)
         kms.append(rk.device_last_kernel_ms())
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t_start
+    ktime = rk.kernel_timing(0)
+    log(f"[rank {rank}] kernel time per class over {args.steps} steps: {ktime}")
 
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if world > 1:
@@ -178,14 +188,23 @@ def main():
 
     roofline = None
     if stats is not None:
-        algo = (BYTES["vol"] * stats["vol"] + BYTES["tri"] * stats["tri"] + BYTES["mat"] * stats["mat"] +
-                BYTES["env"] * stats["env"] + BYTES["cdf"] * stats["cdf"])
-        achieved = algo / (kernel_ms * 1e-3) / 1e9
-        roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": load_traffic(args.config, world),
-                    "algo_bytes_per_launch": algo, "bytes_per_sample": round(algo / (frame.rows * W * spp), 1),
-                    "rays_per_sample": round(stats["rays"] / (frame.rows * W * spp), 3),
-                    "kernel_ms": round(kernel_ms, 3)}
+        dom = max(("trace_closest", "trace_any", "step"), key=lambda k: ktime[k][0])
+        tot_ms, launches = ktime[dom]
+        per_render = algo_bytes(stats, dom)          # the counter pass rendered one frame
+        algo = per_render / max(launches / args.steps, 1)  # per launch
+        avg_ms = tot_ms / max(launches, 1)
+        achieved = algo / (avg_ms * 1e-3) / 1e9
+        samples_rank = frame.rows * W * spp
+        roofline = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                    "traffic": load_traffic(args.config, world),
+                    "algo_bytes_per_launch": round(algo), "avg_launch_ms": round(avg_ms, 4),
+                    "launches_per_step": launches / args.steps,
+                    "kernel_ms_per_step": {k: round(v[0] / args.steps, 2) for k, v in ktime.items()},
+                    "bytes_per_sample_all_kernels": round(sum(algo_bytes(stats, k) for k in ktime) / samples_rank, 1),
+                    "closest_rays_per_sample": round(stats["rays"] / samples_rank, 3),
+                    "any_rays_per_sample": round(stats["any_rays"] / samples_rank, 3),
+                    "render_ms": round(kernel_ms, 3)}
 
     cpu = None
     parity = None

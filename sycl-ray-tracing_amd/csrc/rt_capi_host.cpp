@@ -44,6 +44,15 @@ RtSceneView rt_host_view(const rt_context* c)
     return v;
 }
 
+bool rt_scene_has_emissive_prim(const rt_context* c)
+{
+    for (int32_t mi : c->mat_idx) {
+        const RtMat& m = c->mats[mi];
+        if (m.er > 0 || m.eg > 0 || m.eb > 0) return true;
+    }
+    return false;
+}
+
 extern "C" {
 
 int rt_version(void) { return 10000; }

@@ -55,3 +55,7 @@ int rt_backend_intersect(rt_context* ctx, const float* rays, int n, void* out);
 
 int rt_fail(rt_context* ctx, int code, const std::string& msg);
 RtSceneView rt_host_view(const rt_context* ctx);  // host-memory view (hostsim)
+// Does any primitive (triangle or sphere) use a material with a positive
+// emission component (the test at render_kernel.cpp:696)? If not, the
+// BRDF->light query of sample_light_sources can never contribute.
+bool rt_scene_has_emissive_prim(const rt_context* ctx);

@@ -56,8 +56,10 @@ struct RtCamera {
     float fov_dist;
 };
 
-// Per-launch counters (stats build): rays traced, child-volume tests,
-// triangle tests, leaf visits, material fetches, env texel fetches, CDF probes.
+// Per-render counters (stats build). Closest-hit queries: rays traced,
+// child-volume tests, triangle tests, leaf visits, tie-order slow paths;
+// shading: material fetches, env texel fetches, CDF probes; occlusion
+// (any-hit) queries: rays, volume tests, triangle tests, leaf visits.
 enum {
     RT_STAT_RAYS = 0,
     RT_STAT_VOL,
@@ -67,5 +69,9 @@ enum {
     RT_STAT_ENV,
     RT_STAT_CDF,
     RT_STAT_HEAP_SLOW,
+    RT_STAT_ANY_RAYS,
+    RT_STAT_ANY_VOL,
+    RT_STAT_ANY_TRI,
+    RT_STAT_ANY_LEAF,
     RT_STAT_COUNT
 };

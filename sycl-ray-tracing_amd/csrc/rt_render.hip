@@ -1,18 +1,26 @@
 // rt_render.hip — gfx950 backend of librt_hip.so: device buffers, the
-// render / ray-query kernels and their launches.
+// wavefront render kernels and their launches.
 //
-// Kernel v1 ("megakernel"): one lane per pixel runs RenderKernel::
-// ray_trace_pixel (render_kernel.cpp:75-181) to completion — all samples,
-// all bounces, all five ray queries per bounce — via rt_trace.h, then does the
-// framebuffer accumulate + tone-map in place. The octree walk keeps its
-// explicit stack in private (scratch) memory.
+// A render is a loop of iterations over the in-flight path slots (one slot
+// per pixel of the launch):
+//   k_step          resolve last bounce, consume the continuation query,
+//                   shade the new hit (RNG draws, sampling) or end the
+//                   sample / start the next one; appends the emitted rays to
+//                   five per-kind queues and the live slot to the next
+//                   active list (wave-aggregated atomics, no host round trip)
+//   k_trace_closest continuation, light-shadow and BRDF->light queries
+//                   (exact reference traversal, rt_trace.h trace_closest)
+//   k_trace_any     env-shadow and BRDF->env occlusion queries (trace_any)
+// Queue sizes live in device memory; kernels read them and fetch work in
+// 64-ray tickets, so the host only launches and, every few iterations,
+// reads the live-slot count.
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
 #include <cstring>
 
 #include "rt_context.h"
-#include "rt_trace.h"
+#include "rt_wave.h"
 
 #define HIPCHK(ctx, expr)                                                                         \
     do {                                                                                          \
@@ -23,18 +31,41 @@
 
 namespace {
 
+#define RT_MAX_TIMED_ITERS 16384
+
 struct DevBuf {
     void* p = nullptr;
     size_t bytes = 0;
 };
 
+// counters[] layout (int32)
+enum {
+    C_Q0 = 0,                 // queue sizes, RK_COUNT entries
+    C_TK_CLOSEST = rtk::RK_COUNT,
+    C_TK_ANY,
+    C_TK_STEP,
+    C_ACT0,                   // live-slot counts, double-buffered
+    C_ACT1,
+    C_COUNT
+};
+
 struct Backend {
     DevBuf nodes, tri4, prim2k, mat_idx, mats, emissive, spheres, env, env_lum, cdf;
     DevBuf stats;     // RT_STAT_COUNT u64
-    DevBuf scratch;   // pixel lists / rays / outputs
+    DevBuf wave;      // path state, pending records, results, queues, lists
+    DevBuf counters;  // C_COUNT int32
+    DevBuf xy;        // pixel list (rt_render_pixels)
     DevBuf fb;        // host-fb staging
+    int32_t* h_act = nullptr;  // pinned host copy of a live-slot count
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     RtSceneView view{};
+    int bl_rays = 1, any_rays = 1;
+    int last_iters = 0;
+    // optional per-kernel timing: events around each launch of each class
+    bool timing = false;
+    hipEvent_t tev[4][RT_MAX_TIMED_ITERS] = {};
+    double kms[3] = {0, 0, 0};      // closest, any, step
+    long klaunch[3] = {0, 0, 0};
 };
 
 int ensure(rt_context* c, DevBuf& b, size_t bytes)
@@ -60,44 +91,171 @@ int upload(rt_context* c, DevBuf& b, const std::vector<T>& v)
 
 Backend* be(rt_context* c) { return (Backend*)c->backend; }
 
-// ------------------------------------------------------------------ kernels
-template <bool STATS>
-__global__ __launch_bounds__(256) void k_render(rtk::Ctx C, float4_* __restrict__ fb, int row_offset, int row_stride,
-                                                int rows_local, unsigned long long* __restrict__ stats)
+// ------------------------------------------------------------ wave helpers
+__device__ __forceinline__ int lane_id() { return __lane_id(); }
+
+// Wave-aggregated append: every lane of the wave must call this converged.
+// Returns this lane's slot in the queue whose size lives at *counter.
+__device__ __forceinline__ int wave_append(int32_t* counter, bool want)
 {
-    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx >= rows_local * C.W) return;
-    const int j = idx / C.W;
-    const int x = idx - j * C.W;
-    const int y = row_offset + j * row_stride;
+    const unsigned long long b = __ballot(want);
+    if (b == 0) return -1;
+    const int leader = __ffsll((long long)b) - 1;
+    int base = 0;
+    if (lane_id() == leader) base = atomicAdd(counter, __popcll(b));
+    base = __shfl(base, leader);
+    const unsigned long long lt = (lane_id() == 0) ? 0ull : (b & (~0ull >> (64 - lane_id())));
+    return want ? base + __popcll(lt) : -1;
+}
+
+// One ticket of 64 work items per wave.
+__device__ __forceinline__ int wave_ticket(int32_t* ticket)
+{
+    int base = 0;
+    if (lane_id() == 0) base = atomicAdd(ticket, 64);
+    return __shfl(base, 0);
+}
+
+template <bool STATS>
+__device__ __forceinline__ void flush_stats(const rtk::Stats& st, unsigned long long* out)
+{
+    if (STATS)
+        for (int i = 0; i < RT_STAT_COUNT; i++)
+            if (st.c[i]) atomicAdd(&out[i], st.c[i]);
+}
+
+// ------------------------------------------------------------------ kernels
+// Path init: every slot seeds its RNG and emits its first camera ray.
+__global__ __launch_bounds__(256) void k_init(rtk::WaveView W, int32_t* act_count)
+{
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;  // grid covers whole waves
+    rtk::Emit e;
+    e.mask = 0;
+    e.active = false;
+    if (p < W.n_slots) rtk::path_init(W, p, e);
+#pragma unroll
+    for (int k = 0; k < rtk::RK_COUNT; k++) {
+        const bool want = (e.mask >> k) & 1u;
+        const int i = wave_append(W.counters + C_Q0 + k, want);
+        if (want) W.q[k][i] = e.r[k];
+    }
+    const int a = wave_append(act_count, e.active);
+    if (e.active) W.act_out[a] = p;
+}
+
+template <bool STATS>
+__global__ __launch_bounds__(256) void k_step(rtk::WaveView W, const int32_t* act_in_count, int32_t* act_out_count,
+                                              unsigned long long* stats)
+{
+    const int n = *act_in_count;
+    rtk::Stats st;
+    if (STATS)
+        for (int i = 0; i < RT_STAT_COUNT; i++) st.c[i] = 0;
+    for (;;) {
+        const int base = wave_ticket(W.counters + C_TK_STEP);
+        if (base >= n) break;
+        const int idx = base + lane_id();
+        rtk::Emit e;
+        e.mask = 0;
+        e.active = false;
+        int p = -1;
+        if (idx < n) {
+            p = W.act_in[idx];
+            rtk::path_step(W, p, e, STATS ? &st : nullptr);
+        }
+#pragma unroll
+        for (int k = 0; k < rtk::RK_COUNT; k++) {
+            const bool want = (e.mask >> k) & 1u;
+            const int i = wave_append(W.counters + C_Q0 + k, want);
+            if (want) W.q[k][i] = e.r[k];
+        }
+        const int a = wave_append(act_out_count, e.active);
+        if (e.active) W.act_out[a] = p;
+    }
+    flush_stats<STATS>(st, stats);
+}
+
+template <bool STATS>
+__global__ __launch_bounds__(256) void k_trace_closest(rtk::WaveView W, unsigned long long* stats)
+{
+    const int n0 = W.counters[C_Q0 + rtk::RK_CONT], n1 = W.counters[C_Q0 + rtk::RK_LSH],
+              n2 = W.counters[C_Q0 + rtk::RK_BL];
+    const int total = n0 + n1 + n2;
     rtk::StackEnt stack[RT_STACK_CAP];
     rtk::Stats st;
     if (STATS)
         for (int i = 0; i < RT_STAT_COUNT; i++) st.c[i] = 0;
-    const rtk::Col f = rtk::trace_pixel(C, x, y, stack, STATS ? &st : nullptr);
-    float4_ px = fb[idx];
-    rtk::tonemap_into(&px.x, f);
-    fb[idx] = px;
-    if (STATS)
-        for (int i = 0; i < RT_STAT_COUNT; i++) atomicAdd(&stats[i], st.c[i]);
+    for (;;) {
+        const int base = wave_ticket(W.counters + C_TK_CLOSEST);
+        if (base >= total) break;
+        const int idx = base + lane_id();
+        if (idx < total) {
+            int kind = rtk::RK_CONT, i = idx;
+            if (i >= n0) {
+                i -= n0;
+                kind = rtk::RK_LSH;
+                if (i >= n1) {
+                    i -= n1;
+                    kind = rtk::RK_BL;
+                }
+            }
+            const rtk::RayRec r = W.q[kind][i];
+            const int slot = (int)rt_asuint(r.o.w);
+            float t;
+            int k;
+            rtk::query_closest(W.S, rtk::v3of(r.o), rtk::v3of(r.d), stack, t, k, STATS ? &st : nullptr);
+            if (kind == rtk::RK_CONT) {
+                W.r_cont_t[slot] = t;
+                W.r_cont_k[slot] = k;
+            } else if (kind == rtk::RK_LSH) {
+                W.r_lsh_t[slot] = t;
+            } else {
+                W.r_bl_t[slot] = t;
+                W.r_bl_k[slot] = k;
+            }
+        }
+    }
+    flush_stats<STATS>(st, stats);
 }
 
-template <bool STATS>
-__global__ __launch_bounds__(256) void k_pixels(rtk::Ctx C, const int* __restrict__ xy, float4_* __restrict__ rgba, int n,
-                                                unsigned long long* __restrict__ stats)
+template <bool STATS, bool ANY>
+__global__ __launch_bounds__(256) void k_trace_any(rtk::WaveView W, unsigned long long* stats)
 {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    rtk::StackEnt stack[RT_STACK_CAP];
+    const int n0 = W.counters[C_Q0 + rtk::RK_ESH], n1 = W.counters[C_Q0 + rtk::RK_BENV];
+    const int total = n0 + n1;
+    uint32_t stack[ANY ? RT_STACK_CAP : 1];
+    rtk::StackEnt cstack[ANY ? 1 : RT_STACK_CAP];
     rtk::Stats st;
     if (STATS)
-        for (int k = 0; k < RT_STAT_COUNT; k++) st.c[k] = 0;
-    const rtk::Col f = rtk::trace_pixel(C, xy[2 * i], xy[2 * i + 1], stack, STATS ? &st : nullptr);
-    float4_ px = rgba[i];
-    rtk::tonemap_into(&px.x, f);
-    rgba[i] = px;
-    if (STATS)
-        for (int k = 0; k < RT_STAT_COUNT; k++) atomicAdd(&stats[k], st.c[k]);
+        for (int i = 0; i < RT_STAT_COUNT; i++) st.c[i] = 0;
+    for (;;) {
+        const int base = wave_ticket(W.counters + C_TK_ANY);
+        if (base >= total) break;
+        const int idx = base + lane_id();
+        if (idx < total) {
+            const int kind = idx < n0 ? rtk::RK_ESH : rtk::RK_BENV;
+            const rtk::RayRec r = W.q[kind][idx < n0 ? idx : idx - n0];
+            const int slot = (int)rt_asuint(r.o.w);
+            bool hit;
+            if (ANY) {
+                hit = rtk::trace_any(W.S, rtk::v3of(r.o), rtk::v3of(r.d), stack, STATS ? &st : nullptr);
+            } else {  // analytic spheres present: the reference's exact closest-hit logic
+                float t;
+                int k;
+                rtk::query_closest(W.S, rtk::v3of(r.o), rtk::v3of(r.d), cstack, t, k, STATS ? &st : nullptr);
+                hit = t > 0.0f;
+            }
+            (kind == rtk::RK_ESH ? W.r_esh : W.r_benv)[slot] = hit ? 1 : 0;
+        }
+    }
+    flush_stats<STATS>(st, stats);
+}
+
+__global__ void k_reset(int32_t* counters, int act_slot)
+{
+    const int i = threadIdx.x;
+    if (i < C_ACT0) counters[i] = 0;
+    if (i == 0) counters[act_slot] = 0;
 }
 
 __global__ __launch_bounds__(256) void k_intersect(RtSceneView S, const float* __restrict__ rays, int32_t* __restrict__ out,
@@ -107,24 +265,28 @@ __global__ __launch_bounds__(256) void k_intersect(RtSceneView S, const float* _
     if (i >= n) return;
     rtk::StackEnt stack[RT_STACK_CAP];
     const float* r = rays + 6 * (size_t)i;
+    const rtk::V3 o = rtk::v3(r[0], r[1], r[2]), d = rtk::v3(r[3], r[4], r[5]);
+    float t;
+    int k;
+    rtk::query_closest(S, o, d, stack, t, k, nullptr);
     rtk::Hit h;
-    const bool f = rtk::intersect_scene(S, rtk::v3(r[0], r[1], r[2]), rtk::v3(r[3], r[4], r[5]), stack, h, nullptr);
-    int32_t* o = out + 11 * (size_t)i;
-    o[0] = f ? 1 : 0;
-    o[1] = h.prim;
-    o[2] = (int32_t)rt_asuint(h.t);
-    const bool any = h.t != -1.0f;
-    o[3] = any ? (int32_t)rt_asuint(h.p.x) : 0;
-    o[4] = any ? (int32_t)rt_asuint(h.p.y) : 0;
-    o[5] = any ? (int32_t)rt_asuint(h.p.z) : 0;
-    o[6] = any ? (int32_t)rt_asuint(h.n.x) : 0;
-    o[7] = any ? (int32_t)rt_asuint(h.n.y) : 0;
-    o[8] = any ? (int32_t)rt_asuint(h.n.z) : 0;
-    o[9] = (int32_t)rt_asuint(-1.0f);
-    o[10] = (int32_t)rt_asuint(-1.0f);
+    const bool f = rtk::hit_from(S, o, d, t, k, h);
+    int32_t* ot = out + 11 * (size_t)i;
+    ot[0] = f ? 1 : 0;
+    ot[1] = h.prim;
+    ot[2] = (int32_t)rt_asuint(t);
+    const bool any = t != -1.0f;
+    ot[3] = any ? (int32_t)rt_asuint(h.p.x) : 0;
+    ot[4] = any ? (int32_t)rt_asuint(h.p.y) : 0;
+    ot[5] = any ? (int32_t)rt_asuint(h.p.z) : 0;
+    ot[6] = any ? (int32_t)rt_asuint(h.n.x) : 0;
+    ot[7] = any ? (int32_t)rt_asuint(h.n.y) : 0;
+    ot[8] = any ? (int32_t)rt_asuint(h.n.z) : 0;
+    ot[9] = (int32_t)rt_asuint(-1.0f);
+    ot[10] = (int32_t)rt_asuint(-1.0f);
 }
 
-// libm self-test kernel (tests/test_gpu_libm.py): out[i] = f(in[i])
+// numerics self-test kernel (tests/test_gpu_parity.py): out[i] = f(in[i])
 __global__ void k_libm(int fn, const float* __restrict__ in, const float* __restrict__ in2, float* __restrict__ out, int n)
 {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -141,11 +303,13 @@ __global__ void k_libm(int fn, const float* __restrict__ in, const float* __rest
         case 6: r = rt_atan2f(x, in2[i]); break;
         case 7: r = rt_sqrtf(x); break;
         case 8: r = x / in2[i]; break;
-        default: r = (float)((double)x * 0.31830988618379067154 / (double)in2[i]); break;
+        case 9: r = (float)((double)x * 0.31830988618379067154 / (double)in2[i]); break;
+        default: r = rtk::slab_div(x, 1.0 / (double)in2[i]); break;  // the slab quotient
     }
     out[i] = r;
 }
 
+// ------------------------------------------------------------- wave memory
 }  // namespace
 
 // ------------------------------------------------------------------- hooks
@@ -161,6 +325,7 @@ int rt_backend_create(rt_context* c)
     c->backend = b;
     HIPCHK(c, hipEventCreate(&b->ev0));
     HIPCHK(c, hipEventCreate(&b->ev1));
+    HIPCHK(c, hipHostMalloc((void**)&b->h_act, 16, hipHostMallocDefault));
     return RT_OK;
 }
 
@@ -169,10 +334,14 @@ void rt_backend_destroy(rt_context* c)
     Backend* b = be(c);
     if (!b) return;
     (void)hipSetDevice(c->device);
-    DevBuf* all[] = {&b->nodes, &b->tri4,    &b->prim2k,  &b->mat_idx, &b->mats,    &b->emissive, &b->spheres,
-                     &b->env,   &b->env_lum, &b->cdf,     &b->stats,   &b->scratch, &b->fb};
+    DevBuf* all[] = {&b->nodes, &b->tri4, &b->prim2k, &b->mat_idx, &b->mats, &b->emissive, &b->spheres, &b->env,
+                     &b->env_lum, &b->cdf, &b->stats, &b->wave, &b->counters, &b->xy, &b->fb};
     for (DevBuf* d : all)
         if (d->p) (void)hipFree(d->p);
+    if (b->h_act) (void)hipHostFree(b->h_act);
+    for (auto& row : b->tev)
+        for (hipEvent_t ev : row)
+            if (ev) (void)hipEventDestroy(ev);
     if (b->ev0) (void)hipEventDestroy(b->ev0);
     if (b->ev1) (void)hipEventDestroy(b->ev1);
     delete b;
@@ -189,7 +358,8 @@ int rt_backend_upload(rt_context* c)
         (r = upload(c, b->mats, c->mats)) || (r = upload(c, b->emissive, c->emissive)) ||
         (r = upload(c, b->spheres, c->spheres)) || (r = upload(c, b->env, c->env)) ||
         (r = upload(c, b->env_lum, c->env_lum)) || (r = upload(c, b->cdf, c->cdf)) ||
-        (r = ensure(c, b->stats, RT_STAT_COUNT * sizeof(unsigned long long))))
+        (r = ensure(c, b->stats, RT_STAT_COUNT * sizeof(unsigned long long))) ||
+        (r = ensure(c, b->counters, C_COUNT * sizeof(int32_t))))
         return r;
     RtSceneView v{};
     v.nodes = (const RtNode*)b->nodes.p;
@@ -208,6 +378,106 @@ int rt_backend_upload(rt_context* c)
     v.eh = c->eh;
     v.n_tris = (int)(c->tris.size() / 9);
     b->view = v;
+    b->bl_rays = rt_scene_has_emissive_prim(c) ? 1 : 0;
+    b->any_rays = v.n_spheres == 0 ? 1 : 0;
+    return RT_OK;
+}
+
+// Runs the wavefront loop for n slots of `src` into fb (device, n float4).
+static int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounces, const rtk::PixSrc& src, int n,
+                    float4_* fb, hipStream_t s)
+{
+    if (n <= 0) return RT_OK;
+    rtk::WaveView W{};
+    const size_t need = rtk::wave_carve(nullptr, (size_t)n, W);
+    if (int r = ensure(c, b->wave, need)) return r;
+    rtk::wave_carve((char*)b->wave.p, (size_t)n, W);
+    W.S = b->view;
+    W.cam = c->cam;
+    W.src = src;
+    W.W = w;
+    W.H = h;
+    W.spp = spp;
+    W.bounces = bounces;
+    W.n_slots = n;
+    W.bl_rays = b->bl_rays;
+    W.any_rays = b->any_rays;
+    W.fb = fb;
+    W.counters = (int32_t*)b->counters.p;
+    int32_t* lists[2] = {(int32_t*)W.act_in, W.act_out};
+    int32_t* cnt = (int32_t*)b->counters.p;
+    unsigned long long* stats = (unsigned long long*)b->stats.p;
+    const bool S = c->stats_enabled;
+    if (S) HIPCHK(c, hipMemsetAsync(b->stats.p, 0, b->stats.bytes, s));
+
+    HIPCHK(c, hipMemsetAsync(cnt, 0, C_COUNT * sizeof(int32_t), s));
+    W.act_in = lists[1];
+    W.act_out = lists[0];
+    const int threads = 256;
+    hipLaunchKernelGGL(k_init, dim3((n + threads - 1) / threads), dim3(threads), 0, s, W, cnt + C_ACT0);
+    HIPCHK(c, hipGetLastError());
+
+    int dev_cus = 256;
+    (void)hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, c->device);
+    const int step_blocks = std::min((n + threads - 1) / threads, dev_cus * 8);
+    const int trace_blocks = std::min((3 * n + threads - 1) / threads, dev_cus * 8);
+    const int any_blocks = std::min((2 * n + threads - 1) / threads, dev_cus * 8);
+    // each sample takes at most bounces + 1 iterations; +2 for init / final resolve
+    long max_iters = (long)spp * ((long)bounces + 1) + 2;
+    if (b->timing) {
+        if (max_iters > RT_MAX_TIMED_ITERS) return rt_fail(c, RT_ERR_ARG, "kernel timing: too many iterations");
+        for (int k = 0; k < 4; k++)
+            for (long i = 0; i < max_iters; i++)
+                if (!b->tev[k][i]) HIPCHK(c, hipEventCreate(&b->tev[k][i]));
+    }
+    int it = 0;
+    for (; it < max_iters; it++) {
+        const int cur = it & 1;
+        const bool T = b->timing;
+        if (T) HIPCHK(c, hipEventRecord(b->tev[0][it], s));
+        if (S)
+            hipLaunchKernelGGL(k_trace_closest<true>, dim3(trace_blocks), dim3(threads), 0, s, W, stats);
+        else
+            hipLaunchKernelGGL(k_trace_closest<false>, dim3(trace_blocks), dim3(threads), 0, s, W, stats);
+        if (T) HIPCHK(c, hipEventRecord(b->tev[1][it], s));
+        if (S && W.any_rays)
+            hipLaunchKernelGGL((k_trace_any<true, true>), dim3(any_blocks), dim3(threads), 0, s, W, stats);
+        else if (S)
+            hipLaunchKernelGGL((k_trace_any<true, false>), dim3(any_blocks), dim3(threads), 0, s, W, stats);
+        else if (W.any_rays)
+            hipLaunchKernelGGL((k_trace_any<false, true>), dim3(any_blocks), dim3(threads), 0, s, W, stats);
+        else
+            hipLaunchKernelGGL((k_trace_any<false, false>), dim3(any_blocks), dim3(threads), 0, s, W, stats);
+        if (T) HIPCHK(c, hipEventRecord(b->tev[2][it], s));
+        hipLaunchKernelGGL(k_reset, dim3(1), dim3(64), 0, s, cnt, C_ACT0 + (cur ^ 1));
+        // step: reads the list written last iteration (lists[cur]) -> lists[cur ^ 1]
+        W.act_in = lists[cur];
+        W.act_out = lists[cur ^ 1];
+        if (S)
+            hipLaunchKernelGGL(k_step<true>, dim3(step_blocks), dim3(threads), 0, s, W, cnt + C_ACT0 + cur,
+                               cnt + C_ACT0 + (cur ^ 1), stats);
+        else
+            hipLaunchKernelGGL(k_step<false>, dim3(step_blocks), dim3(threads), 0, s, W, cnt + C_ACT0 + cur,
+                               cnt + C_ACT0 + (cur ^ 1), stats);
+        if (T) HIPCHK(c, hipEventRecord(b->tev[3][it], s));
+        HIPCHK(c, hipGetLastError());
+        if ((it & 7) == 7) {
+            HIPCHK(c, hipMemcpyAsync(b->h_act, cnt + C_ACT0 + (cur ^ 1), 4, hipMemcpyDeviceToHost, s));
+            HIPCHK(c, hipStreamSynchronize(s));
+            if (*b->h_act == 0) break;
+        }
+    }
+    b->last_iters = it + 1;
+    if (b->timing) {  // per-kernel-class time of this render (HIP events on its stream)
+        HIPCHK(c, hipStreamSynchronize(s));
+        for (int i = 0; i < b->last_iters && i < RT_MAX_TIMED_ITERS; i++)
+            for (int k = 0; k < 3; k++) {
+                float ms = 0;
+                HIPCHK(c, hipEventElapsedTime(&ms, b->tev[k][i], b->tev[k + 1][i]));
+                b->kms[k] += ms;
+                b->klaunch[k] += 1;
+            }
+    }
     return RT_OK;
 }
 
@@ -227,24 +497,16 @@ int rt_backend_render(rt_context* c, int w, int h, int spp, int bounces, float* 
     hipStream_t s = (hipStream_t)stream;
     const int rows_local = (h - row_offset + row_stride - 1) / row_stride;
     const size_t npx = (size_t)rows_local * w;
+    if (npx > 0x7fffffff / 8) return rt_fail(c, RT_ERR_ARG, "render: too many pixels for one launch");
     float4_* fb = (float4_*)dev_fb;
     if (host_fb) {
         if (int r = ensure(c, b->fb, npx * sizeof(float4_))) return r;
         fb = (float4_*)b->fb.p;
         HIPCHK(c, hipMemcpyAsync(fb, host_fb, npx * sizeof(float4_), hipMemcpyHostToDevice, s));
     }
-    if (c->stats_enabled) HIPCHK(c, hipMemsetAsync(b->stats.p, 0, b->stats.bytes, s));
-    rtk::Ctx C{b->view, c->cam, w, h, spp, bounces};
-    const int threads = 256;
-    const int blocks = (int)((npx + threads - 1) / threads);
+    rtk::PixSrc src{w, row_offset, row_stride, nullptr};
     HIPCHK(c, hipEventRecord(b->ev0, s));
-    if (c->stats_enabled)
-        hipLaunchKernelGGL(k_render<true>, dim3(blocks), dim3(threads), 0, s, C, fb, row_offset, row_stride, rows_local,
-                           (unsigned long long*)b->stats.p);
-    else
-        hipLaunchKernelGGL(k_render<false>, dim3(blocks), dim3(threads), 0, s, C, fb, row_offset, row_stride,
-                           rows_local, (unsigned long long*)b->stats.p);
-    HIPCHK(c, hipGetLastError());
+    if (int r = run_wave(c, b, w, h, spp, bounces, src, (int)npx, fb, s)) return r;
     HIPCHK(c, hipEventRecord(b->ev1, s));
     if (host_fb) {
         HIPCHK(c, hipMemcpyAsync(host_fb, fb, npx * sizeof(float4_), hipMemcpyDeviceToHost, s));
@@ -253,7 +515,7 @@ int rt_backend_render(rt_context* c, int w, int h, int spp, int bounces, float* 
         HIPCHK(c, hipEventElapsedTime(&ms, b->ev0, b->ev1));
         c->last_kernel_ms = ms;
     } else {
-        c->last_kernel_ms = -1.0;  // read with rt_last_kernel_ms after the caller synchronizes
+        c->last_kernel_ms = -1.0;  // read with rt_device_last_kernel_ms after the caller synchronizes
     }
     return finish_stats(c, b, s);
 }
@@ -263,24 +525,15 @@ int rt_backend_render_pixels(rt_context* c, int w, int h, int spp, int bounces, 
     Backend* b = be(c);
     HIPCHK(c, hipSetDevice(c->device));
     const size_t bxy = (size_t)n * 8, brgba = (size_t)n * 16;
-    if (int r = ensure(c, b->scratch, bxy + brgba)) return r;
-    int* dxy = (int*)b->scratch.p;
-    float4_* drgba = (float4_*)((char*)b->scratch.p + bxy);
-    HIPCHK(c, hipMemcpy(dxy, xy, bxy, hipMemcpyHostToDevice));
-    HIPCHK(c, hipMemcpy(drgba, rgba, brgba, hipMemcpyHostToDevice));
-    if (c->stats_enabled) HIPCHK(c, hipMemset(b->stats.p, 0, b->stats.bytes));
-    rtk::Ctx C{b->view, c->cam, w, h, spp, bounces};
-    const int threads = 256, blocks = (n + threads - 1) / threads;
+    if (int r = ensure(c, b->xy, bxy)) return r;
+    if (int r = ensure(c, b->fb, brgba)) return r;
+    HIPCHK(c, hipMemcpy(b->xy.p, xy, bxy, hipMemcpyHostToDevice));
+    HIPCHK(c, hipMemcpy(b->fb.p, rgba, brgba, hipMemcpyHostToDevice));
+    rtk::PixSrc src{w, 0, 1, (const int32_t*)b->xy.p};
     HIPCHK(c, hipEventRecord(b->ev0, 0));
-    if (c->stats_enabled)
-        hipLaunchKernelGGL(k_pixels<true>, dim3(blocks), dim3(threads), 0, 0, C, dxy, drgba, n,
-                           (unsigned long long*)b->stats.p);
-    else
-        hipLaunchKernelGGL(k_pixels<false>, dim3(blocks), dim3(threads), 0, 0, C, dxy, drgba, n,
-                           (unsigned long long*)b->stats.p);
-    HIPCHK(c, hipGetLastError());
+    if (int r = run_wave(c, b, w, h, spp, bounces, src, n, (float4_*)b->fb.p, 0)) return r;
     HIPCHK(c, hipEventRecord(b->ev1, 0));
-    HIPCHK(c, hipMemcpy(rgba, drgba, brgba, hipMemcpyDeviceToHost));
+    HIPCHK(c, hipMemcpy(rgba, b->fb.p, brgba, hipMemcpyDeviceToHost));
     float ms = 0;
     HIPCHK(c, hipEventElapsedTime(&ms, b->ev0, b->ev1));
     c->last_kernel_ms = ms;
@@ -292,9 +545,9 @@ int rt_backend_intersect(rt_context* c, const float* rays, int n, void* out)
     Backend* b = be(c);
     HIPCHK(c, hipSetDevice(c->device));
     const size_t br = (size_t)n * 24, bo = (size_t)n * 44;
-    if (int r = ensure(c, b->scratch, br + bo)) return r;
-    float* dr = (float*)b->scratch.p;
-    int32_t* dout = (int32_t*)((char*)b->scratch.p + br);
+    if (int r = ensure(c, b->xy, br + bo)) return r;
+    float* dr = (float*)b->xy.p;
+    int32_t* dout = (int32_t*)((char*)b->xy.p + br);
     HIPCHK(c, hipMemcpy(dr, rays, br, hipMemcpyHostToDevice));
     const int threads = 256, blocks = (n + threads - 1) / threads;
     hipLaunchKernelGGL(k_intersect, dim3(blocks), dim3(threads), 0, 0, b->view, dr, dout, n);
@@ -321,14 +574,35 @@ extern "C" int rt_device_libm(int device, int fn, const float* in, const float* 
     return e == hipSuccess ? RT_OK : RT_ERR_HIP;
 }
 
-// Kernel time of the last rt_render_device launch (events recorded on its
-// stream); call after synchronizing that stream.
+// Time between the events around the last rt_render_device launch sequence
+// (recorded on its stream); call after synchronizing that stream.
 extern "C" double rt_device_last_kernel_ms(rt_context* c)
 {
     if (!c || !c->backend) return -1.0;
     Backend* b = be(c);
     float ms = 0;
+    if (hipEventSynchronize(b->ev1) != hipSuccess) return -1.0;
     if (hipEventElapsedTime(&ms, b->ev0, b->ev1) != hipSuccess) return -1.0;
     c->last_kernel_ms = ms;
     return ms;
+}
+
+// Iterations the last wavefront render took.
+extern "C" int rt_device_last_iterations(rt_context* c) { return c && c->backend ? be(c)->last_iters : -1; }
+
+// Per-kernel-class timing (closest-hit trace, occlusion trace, step) over
+// the renders since it was enabled: out_ms[3] total ms, out_launches[3].
+extern "C" int rt_device_kernel_timing(rt_context* c, int enable, double* out_ms, long* out_launches)
+{
+    if (!c || !c->backend) return RT_ERR_ARG;
+    Backend* b = be(c);
+    if (out_ms)
+        for (int k = 0; k < 3; k++) out_ms[k] = b->kms[k];
+    if (out_launches)
+        for (int k = 0; k < 3; k++) out_launches[k] = b->klaunch[k];
+    if (enable >= 0) {
+        b->timing = enable != 0;
+        for (int k = 0; k < 3; k++) b->kms[k] = 0, b->klaunch[k] = 0;
+    }
+    return RT_OK;
 }

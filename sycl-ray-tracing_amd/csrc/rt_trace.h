@@ -1,14 +1,16 @@
-// rt_trace.h — the per-pixel path tracer that runs on gfx950 (and, compiled
-// for the host, in the hostsim test build).
+// rt_trace.h — scene queries and shading primitives of the path tracer that
+// runs on gfx950 (and, compiled for the host, in the hostsim test build).
 //
-// Restates source/render_kernel.cpp (ray_trace_pixel and everything it calls)
+// Restates the functions source/render_kernel.cpp's ray_trace_pixel calls,
 // with the reference's exact float/double evaluation order. Differences are
 // purely structural:
 //  * BVH: the recursive priority-queue octree traversal (bvh.h:127-209) is
 //    re-expressed as an explicit-stack walk over RtNode child blocks that
 //    visits nodes in the identical order (libstdc++ heap tie order included)
 //    and applies the identical early-exit rule; see trace_closest().
+//    Occlusion-only queries use trace_any() (same reachable set, first hit).
 //  * libm: rt_libm.h (glibc-bit-exact).
+// The bounce loop itself lives in rt_wave.h (wavefront form).
 #pragma once
 
 #include "rt_device.h"
@@ -76,31 +78,68 @@ struct Hit {
 
 RT_HD V3 ld3(const float4_& f) { return v3(f.x, f.y, f.z); }
 
-// plane normals (bvh.cpp:8-16)
-#define RT_S3 0.577350269f
-RT_HD void ray_planes(V3 o, V3 d, float* den, float* num)
+// ------------------------------------------------------------- traversal
+#define RT_STACK_CAP 232  // >= 7 * 32 + 1: worst case for an octree of depth 32
+
+struct StackEnt {
+    uint32_t rec;   // record index | FIRST | LAST flags
+    float tnear;
+    int32_t snap;   // leaves visited when the previous sibling was popped
+};
+#define RT_ENT_FIRST 0x80000000u
+#define RT_ENT_LAST 0x40000000u
+#define RT_ENT_MASK 0x3fffffffu
+
+struct Stats {
+    unsigned long long c[RT_STAT_COUNT];
+};
+
+// Per-ray slab constants: den = n.d, num = n.o for the 7 plane normals
+// (bvh.h:133-137) and rinv = 1/(double)den. The slab quotient
+// (d - num) / den is evaluated as (float)((double)(d - num) * rinv): with
+// rinv within 2^-53 of 1/den and one more rounding in the product, the
+// double result is within ~2^-52 (relative) of the exact quotient, while
+// the exact quotient of two floats is never closer than 2^-49 (relative)
+// to a float rounding boundary, so the final rounding to float gives the
+// correctly rounded IEEE f32 quotient — the reference's `/` — for every
+// finite operand (tests: test_gpu_parity.py::test_gpu_slab_division_exact).
+// On gfx950 that is 3 instructions instead of the ~10 of an IEEE f32 divide.
+struct RayK {
+    float den[7], num[7];
+    double rinv[7];
+};
+
+RT_HD float slab_div(float a, double rinv) { return (float)((double)a * rinv); }
+
+RT_HD bool ray_setup(V3 o, V3 d, RayK& k)
 {
     const float s = rt_sqrtf(3.0f) / 3;
     const V3 N[7] = {v3(1, 0, 0), v3(0, 1, 0), v3(0, 0, 1), v3(s, s, s), v3(-s, s, s), v3(-s, -s, s), v3(s, -s, s)};
+    bool bad = false;
 #pragma unroll
     for (int i = 0; i < 7; i++) {
-        den[i] = dot(N[i], d);
-        num[i] = dot(N[i], o);
+        k.den[i] = dot(N[i], d);
+        k.num[i] = dot(N[i], o);
+        k.rinv[i] = 1.0 / (double)k.den[i];
+        bad = bad || rt_isnan(k.den[i]) || rt_isnan(k.num[i]);
     }
+    // A NaN component makes every slab test pass and every triangle test
+    // fail (NaN compares false), so such a ray can never hit.
+    return !bad;
 }
 
 // BoundingVolume::intersect (bounding_volume.h:101-126). The early
 // `t_far < t_near` exit inside the loop cannot change the outcome (prefix
 // max/min are monotone), so the slab loop runs to completion.
-RT_HD bool slab_test(const RtNode& nd, const float* den, const float* num, float& tnear)
+RT_HD bool slab_test(const RtNode& nd, const RayK& k, float& tnear)
 {
     float tn = -__builtin_inff(), tf = __builtin_inff();
 #pragma unroll
     for (int i = 0; i < 7; i++) {
-        const float d = den[i];
+        const float d = k.den[i];
         if (d == 0.0f) continue;
-        float a = (nd.dn[i] - num[i]) / d;
-        float b = (nd.df[i] - num[i]) / d;
+        float a = slab_div(nd.dn[i] - k.num[i], k.rinv[i]);
+        float b = slab_div(nd.df[i] - k.num[i], k.rinv[i]);
         if (d < 0.0f) {
             float t = a;
             a = b;
@@ -190,22 +229,6 @@ RT_HD void heap_order(float* key, int* id, int m, float* okey, int* oid)
     }
 }
 
-// ------------------------------------------------------------- traversal
-#define RT_STACK_CAP 232  // >= 7 * 32 + 1: worst case for an octree of depth 32
-
-struct StackEnt {
-    uint32_t rec;   // record index | FIRST | LAST flags
-    float tnear;
-    int32_t snap;   // leaves visited when the previous sibling was popped
-};
-#define RT_ENT_FIRST 0x80000000u
-#define RT_ENT_LAST 0x40000000u
-#define RT_ENT_MASK 0x3fffffffu
-
-struct Stats {
-    unsigned long long c[RT_STAT_COUNT];
-};
-
 RT_HD void leaf_test(const RtSceneView& S, const RtNode& nd, V3 o, V3 d, float& best_t, int& best_k, Stats* st)
 {
     const int n = (int)(nd.cnt & ~RT_LEAF_BIT);
@@ -230,20 +253,14 @@ RT_HD void trace_closest(const RtSceneView& S, V3 o, V3 d, StackEnt* stack, floa
 {
     best_t = -1.0f;
     best_k = -1;
-    float den[7], num[7];
-    ray_planes(o, d, den, num);
+    RayK K;
     if (st) st->c[RT_STAT_RAYS]++;
-    // A NaN component makes every slab test pass and every triangle test
-    // fail (NaN compares false), so such a ray can never hit: skip the walk.
-    bool bad = false;
-#pragma unroll
-    for (int i = 0; i < 7; i++) bad = bad || rt_isnan(den[i]) || rt_isnan(num[i]);
-    if (bad) return;
+    if (!ray_setup(o, d, K)) return;
 
     const RtNode root = S.nodes[0];
     float tn;
     if (st) st->c[RT_STAT_VOL]++;
-    if (!slab_test(root, den, num, tn)) return;
+    if (!slab_test(root, K, tn)) return;
     if (root.cnt & RT_LEAF_BIT) {
         leaf_test(S, root, o, d, best_t, best_k, st);
         return;
@@ -264,7 +281,7 @@ RT_HD void trace_closest(const RtSceneView& S, V3 o, V3 d, StackEnt* stack, floa
             for (int c = 0; c < nc; c++) {
                 const RtNode ch = S.nodes[base + c];
                 float t;
-                if (slab_test(ch, den, num, t)) {
+                if (slab_test(ch, K, t)) {
                     for (int j = 0; j < m; j++) tie |= (hk[j] == t);
                     hk[m] = t;
                     hi[m] = base + c;
@@ -329,6 +346,45 @@ RT_HD void trace_closest(const RtSceneView& S, V3 o, V3 d, StackEnt* stack, floa
     }
 }
 
+// Occlusion query: does the reference's traversal find ANY triangle hit?
+// Pruning in BVH::intersect is by slab tests (independent of the hit state)
+// and by the early exit, which only fires once a hit exists; so the
+// reference finds a hit iff some leaf reachable through passing slab tests
+// holds a triangle the ray hits. This walk visits that same reachable set
+// in child order (no sorting) and stops at the first hit.
+RT_HD bool trace_any(const RtSceneView& S, V3 o, V3 d, uint32_t* stack, Stats* st)
+{
+    RayK K;
+    if (st) st->c[RT_STAT_ANY_RAYS]++;
+    if (!ray_setup(o, d, K)) return false;
+    float tn;
+    if (st) st->c[RT_STAT_ANY_VOL]++;
+    if (!slab_test(S.nodes[0], K, tn)) return false;
+    int sp = 0;
+    stack[sp++] = 0;
+    while (sp > 0) {
+        const RtNode nd = S.nodes[stack[--sp]];
+        if (nd.cnt & RT_LEAF_BIT) {
+            const int n = (int)(nd.cnt & ~RT_LEAF_BIT);
+            if (st) {
+                st->c[RT_STAT_ANY_TRI] += n;
+                st->c[RT_STAT_ANY_LEAF] += 1;
+            }
+            for (int j = 0; j < n; j++) {
+                float t;
+                if (tri_test(S.tri4, (int)nd.ref + j, o, d, t)) return true;
+            }
+            continue;
+        }
+        const int base = (int)nd.ref, nc = (int)nd.cnt;
+        if (st) st->c[RT_STAT_ANY_VOL] += nc;
+        for (int c = nc - 1; c >= 0; c--) {
+            if (slab_test(S.nodes[base + c], K, tn)) stack[sp++] = (uint32_t)(base + c);
+        }
+    }
+    return false;
+}
+
 // Sphere::intersect (sphere.h:11-52)
 RT_HD bool sphere_test(const float4_* sp, int i, V3 o, V3 d, Hit& h)
 {
@@ -357,30 +413,6 @@ RT_HD bool sphere_test(const float4_* sp, int i, V3 o, V3 d, Hit& h)
     h.prim = rt_asuint(sp[2 * i + 1].x);
     h.k = -2 - i;
     return true;
-}
-
-// INTERSECT_SCENE = intersect_scene_bvh (render_kernel.cpp:485-502)
-RT_HD bool intersect_scene(const RtSceneView& S, V3 o, V3 d, StackEnt* stack, Hit& h, Stats* st)
-{
-    float t;
-    int k;
-    trace_closest(S, o, d, stack, t, k, st);
-    h.t = t;
-    h.k = k;
-    h.prim = -1;
-    if (k >= 0) {
-        // HitInfo fields of the winning Triangle::intersect (triangle.h:46-56)
-        const V3 e1 = ld3(S.tri4[3 * k + 1]), e2 = ld3(S.tri4[3 * k + 2]);
-        h.p = add(o, mul(t, d));
-        h.n = normalize(cross(e1, e2));
-        h.prim = (int)rt_asuint(S.tri4[3 * k].w);
-    }
-    for (int i = 0; i < S.n_spheres; i++) {
-        Hit sh;
-        if (sphere_test(S.spheres, i, o, d, sh))
-            if (sh.t < h.t || h.t == -1.0f) h = sh;
-    }
-    return h.t > 0.0f;
 }
 
 // ----------------------------------------------------------------- shading
@@ -536,221 +568,6 @@ RT_HD void cdf_search(const RtSceneView& S, float value, int& x, int& y, Stats* 
     }
     x = rt_maxi(rt_mini(lower, S.ew), 0);
     if (st) st->c[RT_STAT_CDF] += probes;
-}
-
-struct Ctx {
-    RtSceneView S;
-    RtCamera cam;
-    int W, H, spp, bounces;
-};
-
-RT_HD bool occluded(const Ctx& C, V3 o, V3 d, StackEnt* stack, Stats* st)
-{
-    Hit h;
-    return intersect_scene(C.S, o, d, stack, h, st);
-}
-
-RT_HD Col sample_env(const Ctx& C, V3 rd, const Hit& h, const Mat& m, Rng& rng, StackEnt* stack, Stats* st)
-{
-    const RtSceneView& S = C.S;
-    const float total = S.cdf[S.ew * S.eh - 1];
-    int x, y;
-    cdf_search(S, rng.next() * total, x, y, st);
-    float u = (float)x / (float)S.ew, v = (float)y / (float)S.eh;
-    float phi = (float)((double)(u * 2.0f) * 3.14159265358979323846);
-    float theta = (float)((double)v * 3.14159265358979323846);
-    Col env_sample = col(0.0f);
-    float st_ = rt_sinf(theta), ct_ = rt_cosf(theta);
-    V3 dir = v3(-st_ * rt_cosf(phi), -ct_, -st_ * rt_sinf(phi));
-    float cosine = dot(h.n, dir);
-    if (cosine > 0.0f) {
-        if (!occluded(C, add(h.p, mul(1.0e-4f, h.n)), dir, stack, st)) {
-            float pdf = S.env_lum[y * S.ew + x] / total;
-            pdf = (float)((double)((pdf * (float)S.ew) * (float)S.eh) /
-                          (2.0 * 3.14159265358979323846 * 3.14159265358979323846 * (double)st_));
-            Col rad = env_texel(S, x, y, st);
-            Col brdf = ct_brdf(m, dir, neg(rd), h.n);
-            float bp = ct_pdf(m, neg(rd), dir, h.n);
-            float mis = power_heuristic(pdf, bp);
-            env_sample = cdiv(cmul(cscale(cscale(brdf, cosine), mis), rad), pdf);
-        }
-    }
-    float bsp;
-    V3 bdir = v3(0.0f, 0.0f, 0.0f);
-    Col bis = ct_sample(m, neg(rd), h.n, bdir, bsp, rng);
-    cosine = rt_max(dot(h.n, bdir), 0.0f);
-    Col brdf_sample = col(0.0f);
-    if (bsp != 0.0f && cosine > 0.0f) {
-        if (!occluded(C, add(h.p, mul(1.0e-5f, h.n)), bdir, stack, st)) {
-            Col sky = env_from_dir(S, bdir, st);
-            float th = rt_acosf(bdir.z);
-            float sth = rt_sinf(th);
-            float epdf = (0.3086f * sky.r + 0.6094f * sky.g + 0.0820f * sky.b) / S.cdf[S.ew * S.eh - 1];
-            epdf *= (float)(S.ew * S.eh);
-            epdf = (float)((double)epdf / (2.0 * 3.14159265358979323846 * 3.14159265358979323846 * (double)sth));
-            float mis = power_heuristic(bsp, epdf);
-            brdf_sample = cdiv(cmul(cscale(cscale(sky, mis), cosine), bis), bsp);
-        }
-    }
-    return cadd(brdf_sample, env_sample);
-}
-
-RT_HD Col sample_lights(const Ctx& C, V3 rd, const Hit& h, const Mat& m, Rng& rng, StackEnt* stack, Stats* st)
-{
-    const RtSceneView& S = C.S;
-    Col light = col(0.0f);
-    if (S.n_emissive > 0) {
-        // sample_random_point_on_lights (:715-742)
-        int li = rt_f2i(rng.next() * (float)S.n_emissive);
-        li = S.emissive[li];
-        const int lk = S.prim2k[li];
-        const V3 A = ld3(S.tri4[3 * lk]), AB = ld3(S.tri4[3 * lk + 1]), AC = ld3(S.tri4[3 * lk + 2]);
-        float r1 = rng.next();
-        float r2 = rng.next();
-        float sr1 = rt_sqrtf(r1);
-        float u = 1.0f - sr1, v = (1.0f - r2) * sr1;
-        V3 P = add(add(A, mul(u, AB)), mul(v, AC));
-        V3 nrm = cross(AB, AC);
-        float ln = length(nrm);
-        V3 lnorm = mul(1 / ln, nrm);
-        float area = ln * 0.5f;
-        float nb = (float)S.n_emissive;
-        float lpdf = 1.0f / (nb * area);
-
-        V3 so = add(h.p, mul(1.0e-4f, h.n));
-        V3 sd = sub(P, so);
-        float dist = length(sd);
-        V3 sdn = normalize(sd);
-        float dl = rt_max(dot(lnorm, neg(sdn)), 0.0f);
-        if (dl > 0.0f) {
-            Hit sh;  // evaluate_shadow_ray (:744-759)
-            bool in_shadow = false;
-            if (intersect_scene(S, so, sdn, stack, sh, st)) in_shadow = sh.t + 1.0e-4f < dist;
-            if (!in_shadow) {
-                if (st) st->c[RT_STAT_MAT]++;
-                const Mat em = load_mat(S, li);
-                lpdf *= dist * dist;
-                lpdf /= dl;
-                Col brdf = ct_brdf(m, sdn, neg(rd), h.n);
-                float cp = ct_pdf(m, neg(rd), sdn, h.n);
-                if (cp != 0.0f) {
-                    float mis = power_heuristic(lpdf, cp);
-                    float cosine = dot(h.n, sdn);
-                    light = cdiv(cscale(cmul(cscale(em.emission, cosine), brdf), mis), lpdf);
-                }
-            }
-        }
-    }
-    Col bmis = col(0.0f);
-    V3 sdir = v3(0.0f, 0.0f, 0.0f);
-    float dpdf;
-    Col brdf = ct_sample(m, neg(rd), h.n, sdir, dpdf, rng);
-    if (!(brdf.r == 0.0f && brdf.g == 0.0f && brdf.b == 0.0f)) {
-        Hit nh;
-        if (intersect_scene(S, add(h.p, mul(1.0e-5f, h.n)), sdir, stack, nh, st)) {
-            float ca = rt_max(dot(nh.n, neg(sdir)), 0.0f);
-            if (ca > 0.0f) {
-                if (st) st->c[RT_STAT_MAT]++;
-                const Mat mm = load_mat(S, nh.prim);
-                const Col e = mm.emission;
-                if (e.r > 0 || e.g > 0 || e.b > 0) {
-                    float d2 = nh.t * nh.t;
-                    // Triangle::area (triangle.cpp:8-11) of the hit triangle
-                    // (an emissive *sphere* hit reads past the triangle buffer in the
-                    // reference — undefined behaviour; we use area 0 there)
-                    const int kk = nh.k >= 0 ? nh.k : (nh.prim >= 0 && nh.prim < S.n_tris ? S.prim2k[nh.prim] : -1);
-                    float la = kk < 0 ? 0.0f : length(cross(ld3(S.tri4[3 * kk + 1]), ld3(S.tri4[3 * kk + 2]))) / 2;
-                    float lp = d2 / (la * ca);
-                    float mis = power_heuristic(dpdf, lp);
-                    float cosine = dot(h.n, sdir);
-                    bmis = cdiv(cscale(cmul(cscale(brdf, cosine), e), mis), dpdf);
-                }
-            }
-        }
-    }
-    return cadd(light, bmis);
-}
-
-RT_HD V3 xform_point(const RtCamera& c, V3 p)  // mat.cpp:94-111
-{
-    const float* m = c.m;
-    float xt = m[0] * p.x + m[1] * p.y + m[2] * p.z + m[3];
-    float yt = m[4] * p.x + m[5] * p.y + m[6] * p.z + m[7];
-    float zt = m[8] * p.x + m[9] * p.y + m[10] * p.z + m[11];
-    float wt = m[12] * p.x + m[13] * p.y + m[14] * p.z + m[15];
-    float w = 1.f / wt;
-    if (wt == 1.f) return v3(xt, yt, zt);
-    return v3(xt * w, yt * w, zt * w);
-}
-
-// RenderKernel::ray_trace_pixel (render_kernel.cpp:75-181): returns the
-// HDR pixel colour `final_color` (before it is added to the framebuffer).
-RT_HD Col trace_pixel(const Ctx& C, int x, int y, StackEnt* stack, Stats* st)
-{
-    const RtSceneView& S = C.S;
-    Rng rng{(uint32_t)(31 + x * y * C.spp)};
-    for (int i = 0; i < 10; i++) rng.next();
-    Col fin = col(0.0f);
-    const V3 o = xform_point(C.cam, v3(0.0f, 0.0f, 0.0f));
-    for (int s = 0; s < C.spp; s++) {
-        float xj = ((float)x + 0.5f) + rng.next() - 1.0f;
-        float yj = ((float)y + 0.5f) + rng.next() - 1.0f;
-        // get_camera_ray (:56-73)
-        float xn = xj / (float)C.W * 2.0f - 1.0f;
-        xn *= (float)C.W / (float)C.H;
-        float yn = yj / (float)C.H * 2.0f - 1.0f;
-        V3 pd = xform_point(C.cam, v3(xn, yn, C.cam.fov_dist));
-        V3 ro = o, rd = normalize(sub(pd, o));
-        Col thr = col(1.0f), sc = col(0.0f);
-        int state = 0;  // 0 BOUNCE, 1 MISSED
-        for (int bounce = 0; bounce < C.bounces; bounce++) {
-            if (state == 0) {
-                Hit h;
-                if (intersect_scene(S, ro, rd, stack, h, st)) {
-                    if (st) st->c[RT_STAT_MAT]++;
-                    const Mat m = load_mat(S, h.prim);
-                    Col lr = sample_lights(C, rd, h, m, rng, stack, st);
-                    Col er = sample_env(C, rd, h, m, rng, stack, st);
-                    float bpdf;
-                    V3 dir = v3(0.0f, 0.0f, 0.0f);
-                    Col brdf = ct_sample(m, neg(rd), h.n, dir, bpdf, rng);
-                    if (bounce == 0) sc = cadd(sc, m.emission);
-                    sc = cadd(sc, cmul(cadd(lr, er), thr));
-                    if ((brdf.r == 0.0f && brdf.g == 0.0f && brdf.b == 0.0f) || bpdf < 1.0e-8f || rt_isinf(bpdf))
-                        break;
-                    thr = cmul(thr, cdiv(cscale(brdf, rt_max(0.0f, dot(dir, h.n))), bpdf));
-                    ro = add(h.p, mul(1.0e-4f, h.n));
-                    rd = dir;
-                } else
-                    state = 1;
-            } else {
-                if (bounce == 1) sc = cadd(sc, cmul(env_from_dir(S, rd, st), thr));
-                break;
-            }
-        }
-        fin = cadd(fin, sc);
-    }
-    const float k = (float)C.spp;
-    fin.r /= k;
-    fin.g /= k;
-    fin.b /= k;
-    return fin;
-}
-
-// framebuffer update + exposure / gamma tone-map (:167-180), in place.
-RT_HD void tonemap_into(float* px, Col fin)
-{
-    px[0] += fin.r;
-    px[1] += fin.g;
-    px[2] += fin.b;
-    const float a = px[3] + 0.0f;
-    px[3] = 1.0f + (-((-a) * 1.5f));
-#pragma unroll
-    for (int c = 0; c < 3; c++) {
-        float e = rt_expf((-px[c]) * 1.5f);
-        float tm = 1.0f + (-e);
-        px[c] = rt_powf(tm, 1.0f / 2.2f);
-    }
 }
 
 }  // namespace rtk

@@ -1,0 +1,545 @@
+// rt_wave.h — the wavefront form of RenderKernel::ray_trace_pixel
+// (render_kernel.cpp:75-181), shared by the gfx950 kernels (rt_render.hip)
+// and the CPU build of the same code (rt_hostsim.cpp).
+//
+// Why a wavefront: a bounce of the reference issues up to five scene
+// queries (continuation, light shadow, BRDF->light, env shadow, BRDF->env),
+// but every RNG draw of the bounce happens before any of them is looked at
+// and no query's origin or direction depends on another query's result. So
+// one bounce splits into
+//   shade    (RNG draws, BRDF / env / light sampling; emits the rays),
+//   trace    (closest-hit / occlusion queries, separate kernels),
+//   resolve  (the reference's arithmetic on the query results, in its order).
+// Every path keeps its RNG state, so each pixel's draws happen in exactly
+// the reference's order; pixels are independent, so running them side by
+// side changes nothing. The per-path loop below is an exact re-expression of
+// the reference's bounce loop, state machine included (MISSED, bounce==1 sky
+// rule, emission at bounce 0, `break` on a dead BRDF sample).
+//
+// Buffers (device memory, one entry per path slot; slot = pixel index of
+// the launch's pixel source): 16-B records so a wave's loads coalesce.
+#pragma once
+
+#include "rt_trace.h"
+
+namespace rtk {
+
+enum RayKind { RK_CONT = 0, RK_LSH = 1, RK_BL = 2, RK_ESH = 3, RK_BENV = 4, RK_COUNT = 5 };
+
+enum PathFlag : uint32_t {
+    PF_CONT = 1u,        // a continuation / camera ray is in flight
+    PF_END = 2u,         // the sample ends once the pending bounce is resolved
+    PF_AUX = 4u,         // a shaded bounce waits to be resolved
+    PF_LSH = 8u,         // light shadow ray emitted (and its candidate is valid)
+    PF_BL = 16u,         // BRDF->light ray emitted
+    PF_ESH = 32u,        // env shadow ray emitted
+    PF_BENV = 64u,       // BRDF->env ray emitted
+    PF_EMIT0 = 128u,     // bounce 0: add the material emission at resolve
+};
+
+struct RayRec {  // 32 B queue entry
+    float4_ o;  // xyz origin, w = target (slot) bits
+    float4_ d;  // xyz direction
+};
+
+// Pixel source of a launch: image rows y = off + j*stride (j = slot / W), or
+// an explicit (x, y) list (ray_trace_pixel over a pixel set).
+struct PixSrc {
+    int W, off, stride;
+    const int32_t* xy;
+};
+
+RT_HD void pix_xy(const PixSrc& src, int i, int& x, int& y)
+{
+    if (src.xy) {
+        x = src.xy[2 * i];
+        y = src.xy[2 * i + 1];
+    } else {
+        const int j = i / src.W;
+        x = i - j * src.W;
+        y = src.off + j * src.stride;
+    }
+}
+
+struct WaveView {
+    RtSceneView S;
+    RtCamera cam;
+    PixSrc src;
+    int W, H, spp, bounces;
+    int n_slots;
+    int bl_rays;            // 0: no primitive has an emissive material -> BRDF->light rays can't contribute
+    int any_rays;           // 1: occlusion queries may use the any-hit walk (no analytic spheres)
+    float4_* fb;            // [n_slots] framebuffer values (read-modify-write at pixel end)
+    // path state
+    float4_* p_ro;          // ro.xyz, rng bits
+    float4_* p_rd;          // rd.xyz, flags | bounce << 8
+    float4_* p_thr;         // thr.rgb, sample
+    float4_* p_sc;          // sc.rgb
+    float4_* p_fin;         // fin.rgb
+    // pending bounce (shade -> resolve)
+    float4_* q_light;       // light candidate rgb, dist
+    float4_* q_bl;          // BRDF->light sample brdf rgb, pdf
+    float4_* q_sdir;        // BRDF->light dir xyz
+    float4_* q_blo;         // BRDF->light origin xyz (sphere hit normals)
+    float4_* q_hn;          // hit normal xyz
+    float4_* q_env;         // env candidate rgb
+    float4_* q_benv;        // BRDF->env candidate rgb
+    float4_* q_em;          // emission rgb (bounce 0)
+    float4_* q_thr;         // thr at the shaded bounce
+    // query results
+    float* r_cont_t;
+    int32_t* r_cont_k;
+    float* r_lsh_t;
+    float* r_bl_t;
+    int32_t* r_bl_k;
+    uint8_t* r_esh;
+    uint8_t* r_benv;
+    // queues
+    RayRec* q[RK_COUNT];    // [n_slots] each
+    int32_t* counters;      // [RK_COUNT] queue sizes, [RK_COUNT] = next active count
+    const int32_t* act_in;  // active slots this iteration
+    int32_t* act_out;
+    int n_act_in;
+};
+
+// Carves the path-slot buffers for n slots out of one allocation at `base`
+// (nullptr: only sizes it). Returns the bytes needed.
+inline size_t wave_carve(char* base, size_t n, WaveView& W)
+{
+    size_t o = 0;
+    auto take = [&](size_t bytes) -> void* {
+        void* p = base ? base + o : nullptr;
+        o += (bytes + 255) & ~(size_t)255;
+        return p;
+    };
+    W.p_ro = (float4_*)take(n * 16);
+    W.p_rd = (float4_*)take(n * 16);
+    W.p_thr = (float4_*)take(n * 16);
+    W.p_sc = (float4_*)take(n * 16);
+    W.p_fin = (float4_*)take(n * 16);
+    W.q_light = (float4_*)take(n * 16);
+    W.q_bl = (float4_*)take(n * 16);
+    W.q_sdir = (float4_*)take(n * 16);
+    W.q_blo = (float4_*)take(n * 16);
+    W.q_hn = (float4_*)take(n * 16);
+    W.q_env = (float4_*)take(n * 16);
+    W.q_benv = (float4_*)take(n * 16);
+    W.q_em = (float4_*)take(n * 16);
+    W.q_thr = (float4_*)take(n * 16);
+    W.r_cont_t = (float*)take(n * 4);
+    W.r_cont_k = (int32_t*)take(n * 4);
+    W.r_lsh_t = (float*)take(n * 4);
+    W.r_bl_t = (float*)take(n * 4);
+    W.r_bl_k = (int32_t*)take(n * 4);
+    W.r_esh = (uint8_t*)take(n);
+    W.r_benv = (uint8_t*)take(n);
+    for (int k = 0; k < RK_COUNT; k++) W.q[k] = (RayRec*)take(n * sizeof(RayRec));
+    W.act_in = (const int32_t*)take(n * 4);
+    W.act_out = (int32_t*)take(n * 4);
+    return o;
+}
+
+RT_HD float4_ f4(V3 v, float w) { return float4_{v.x, v.y, v.z, w}; }
+RT_HD float4_ f4(Col c, float w) { return float4_{c.r, c.g, c.b, w}; }
+RT_HD V3 v3of(const float4_& f) { return v3(f.x, f.y, f.z); }
+RT_HD Col colof(const float4_& f) { return Col{f.x, f.y, f.z}; }
+
+// What one path step hands to the queues.
+struct Emit {
+    RayRec r[RK_COUNT];
+    uint32_t mask;  // bit k: a ray of kind k
+    bool active;    // the path stays in flight
+};
+
+RT_HD void emit(Emit& e, int kind, int slot, V3 o, V3 d)
+{
+    e.r[kind].o = f4(o, rt_asfloat((uint32_t)slot));
+    e.r[kind].d = f4(d, 0.0f);
+    e.mask |= 1u << kind;
+}
+
+RT_HD V3 xform_point(const RtCamera& c, V3 p)  // mat.cpp:94-111
+{
+    const float* m = c.m;
+    float xt = m[0] * p.x + m[1] * p.y + m[2] * p.z + m[3];
+    float yt = m[4] * p.x + m[5] * p.y + m[6] * p.z + m[7];
+    float zt = m[8] * p.x + m[9] * p.y + m[10] * p.z + m[11];
+    float wt = m[12] * p.x + m[13] * p.y + m[14] * p.z + m[15];
+    float w = 1.f / wt;
+    if (wt == 1.f) return v3(xt, yt, zt);
+    return v3(xt * w, yt * w, zt * w);
+}
+
+// framebuffer update + exposure / gamma tone-map (:167-180), in place.
+RT_HD void tonemap_into(float* px, Col fin)
+{
+    px[0] += fin.r;
+    px[1] += fin.g;
+    px[2] += fin.b;
+    const float a = px[3] + 0.0f;
+    px[3] = 1.0f + (-((-a) * 1.5f));
+#pragma unroll
+    for (int c = 0; c < 3; c++) {
+        float e = rt_expf((-px[c]) * 1.5f);
+        float tm = 1.0f + (-e);
+        px[c] = rt_powf(tm, 1.0f / 2.2f);
+    }
+}
+
+// Register copy of one path slot.
+struct PathReg {
+    V3 ro, rd;
+    Rng rng;
+    uint32_t flags;
+    int bounce, sample;
+    Col thr, sc, fin;
+};
+
+RT_HD void load_path(const WaveView& W, int p, PathReg& P)
+{
+    const float4_ a = W.p_ro[p], b = W.p_rd[p], c = W.p_thr[p], d = W.p_sc[p], e = W.p_fin[p];
+    P.ro = v3of(a);
+    P.rng.a = rt_asuint(a.w);
+    P.rd = v3of(b);
+    const uint32_t fb = rt_asuint(b.w);
+    P.flags = fb & 0xffu;
+    P.bounce = (int)(fb >> 8);
+    P.thr = colof(c);
+    P.sample = (int)rt_asuint(c.w);
+    P.sc = colof(d);
+    P.fin = colof(e);
+}
+
+RT_HD void store_path(const WaveView& W, int p, const PathReg& P)
+{
+    W.p_ro[p] = f4(P.ro, rt_asfloat(P.rng.a));
+    W.p_rd[p] = f4(P.rd, rt_asfloat(P.flags | ((uint32_t)P.bounce << 8)));
+    W.p_thr[p] = f4(P.thr, rt_asfloat((uint32_t)P.sample));
+    W.p_sc[p] = f4(P.sc, 0.0f);
+    W.p_fin[p] = f4(P.fin, 0.0f);
+}
+
+// Camera ray of the next sample (render_kernel.cpp:88-92, get_camera_ray
+// :56-73). Returns false when the pixel is complete (then fb is written).
+// With max_bounces == 0 the reference's bounce loop never runs: each sample
+// only draws its 2 jitter values and adds black.
+RT_HD bool start_sample(const WaveView& W, int p, PathReg& P, Emit& e)
+{
+    int x, y;
+    pix_xy(W.src, p, x, y);
+    for (;;) {
+        float xj = ((float)x + 0.5f) + P.rng.next() - 1.0f;
+        float yj = ((float)y + 0.5f) + P.rng.next() - 1.0f;
+        float xn = xj / (float)W.W * 2.0f - 1.0f;
+        xn *= (float)W.W / (float)W.H;
+        float yn = yj / (float)W.H * 2.0f - 1.0f;
+        const V3 o = xform_point(W.cam, v3(0.0f, 0.0f, 0.0f));
+        const V3 pd = xform_point(W.cam, v3(xn, yn, W.cam.fov_dist));
+        P.ro = o;
+        P.rd = normalize(sub(pd, o));
+        P.thr = col(1.0f);
+        P.sc = col(0.0f);
+        P.bounce = 0;
+        P.flags = 0;
+        if (W.bounces > 0) {
+            P.flags = PF_CONT;
+            emit(e, RK_CONT, p, P.ro, P.rd);
+            return true;
+        }
+        P.fin = cadd(P.fin, P.sc);
+        if (++P.sample == W.spp) return false;
+    }
+}
+
+RT_HD void finish_pixel(const WaveView& W, int p, PathReg& P)
+{
+    const float k = (float)W.spp;
+    Col fin = P.fin;
+    fin.r /= k;  // Color /= float is a true division (color.h:69-76)
+    fin.g /= k;
+    fin.b /= k;
+    float4_ px = W.fb[p];
+    tonemap_into(&px.x, fin);
+    W.fb[p] = px;
+}
+
+// Path initialisation: seed + 10 warm-up draws (render_kernel.cpp:77-82),
+// first camera ray.
+RT_HD void path_init(const WaveView& W, int p, Emit& e)
+{
+    int x, y;
+    pix_xy(W.src, p, x, y);
+    PathReg P;
+    P.rng.a = (uint32_t)(31 + x * y * W.spp);
+    for (int i = 0; i < 10; i++) P.rng.next();
+    P.fin = col(0.0f);
+    P.sample = 0;
+    e.mask = 0;
+    e.active = start_sample(W, p, P, e);
+    if (!e.active) finish_pixel(W, p, P);
+    store_path(W, p, P);
+}
+
+// Hit record of a closest-hit query (HitInfo fields the integrator reads).
+RT_HD bool hit_from(const RtSceneView& S, V3 o, V3 d, float t, int k, Hit& h)
+{
+    h.t = t;
+    h.k = k;
+    h.prim = -1;
+    if (k >= 0) {  // triangle (triangle.h:46-56)
+        const V3 e1 = ld3(S.tri4[3 * k + 1]), e2 = ld3(S.tri4[3 * k + 2]);
+        h.p = add(o, mul(t, d));
+        h.n = normalize(cross(e1, e2));
+        h.prim = (int)rt_asuint(S.tri4[3 * k].w);
+    } else if (k <= -2) {  // sphere (sphere.h:46-48)
+        const float4_ s0 = S.spheres[2 * (-2 - k)];
+        h.p = add(o, mul(t, d));
+        h.n = normalize(sub(h.p, ld3(s0)));
+        h.prim = (int)rt_asuint(S.spheres[2 * (-2 - k) + 1].x);
+    }
+    return t > 0.0f;
+}
+
+// ---------------------------------------------------------------- shade
+// The pre-query half of one hit bounce: sample_lights (:633-713),
+// sample_environment_map (:569-631) and the continuation sample (:123),
+// with every RNG draw in the reference's order. Candidate contributions
+// are computed now (they depend only on the draws); resolve() decides with
+// the query results whether they count.
+RT_HD void shade(const WaveView& W, int p, PathReg& P, const Hit& h, Emit& e, Stats* st)
+{
+    const RtSceneView& S = W.S;
+    if (st) st->c[RT_STAT_MAT]++;
+    const Mat m = load_mat(S, h.prim);
+    const V3 rd = P.rd;
+    uint32_t fl = PF_AUX;
+
+    // ---- sample_lights, light half (sample_random_point_on_lights :715-742)
+    if (S.n_emissive > 0) {
+        int li = rt_f2i(P.rng.next() * (float)S.n_emissive);
+        li = S.emissive[li];
+        const int lk = S.prim2k[li];
+        const V3 A = ld3(S.tri4[3 * lk]), AB = ld3(S.tri4[3 * lk + 1]), AC = ld3(S.tri4[3 * lk + 2]);
+        float r1 = P.rng.next();
+        float r2 = P.rng.next();
+        float sr1 = rt_sqrtf(r1);
+        float u = 1.0f - sr1, v = (1.0f - r2) * sr1;
+        V3 Pt = add(add(A, mul(u, AB)), mul(v, AC));
+        V3 nrm = cross(AB, AC);
+        float ln = length(nrm);
+        V3 lnorm = mul(1 / ln, nrm);
+        float area = ln * 0.5f;
+        float nb = (float)S.n_emissive;
+        float lpdf = 1.0f / (nb * area);
+
+        V3 so = add(h.p, mul(1.0e-4f, h.n));
+        V3 sd = sub(Pt, so);
+        float dist = length(sd);
+        V3 sdn = normalize(sd);
+        float dl = rt_max(dot(lnorm, neg(sdn)), 0.0f);
+        if (dl > 0.0f) {
+            // evaluate_shadow_ray (:744-759) is the query; the rest only runs if unshadowed
+            if (st) st->c[RT_STAT_MAT]++;
+            const Mat em = load_mat(S, li);
+            lpdf *= dist * dist;
+            lpdf /= dl;
+            Col brdf = ct_brdf(m, sdn, neg(rd), h.n);
+            float cp = ct_pdf(m, neg(rd), sdn, h.n);
+            if (cp != 0.0f) {
+                float mis = power_heuristic(lpdf, cp);
+                float cosine = dot(h.n, sdn);
+                Col light = cdiv(cscale(cmul(cscale(em.emission, cosine), brdf), mis), lpdf);
+                W.q_light[p] = f4(light, dist);
+                fl |= PF_LSH;
+                emit(e, RK_LSH, p, so, sdn);
+            }
+        }
+    }
+    // ---- sample_lights, BRDF half (:681-711)
+    {
+        V3 sdir = v3(0.0f, 0.0f, 0.0f);
+        float dpdf;
+        Col brdf = ct_sample(m, neg(rd), h.n, sdir, dpdf, P.rng);
+        if (!(brdf.r == 0.0f && brdf.g == 0.0f && brdf.b == 0.0f) && W.bl_rays) {
+            W.q_bl[p] = f4(brdf, dpdf);
+            const V3 blo = add(h.p, mul(1.0e-5f, h.n));
+            W.q_sdir[p] = f4(sdir, 0.0f);
+            W.q_blo[p] = f4(blo, 0.0f);
+            fl |= PF_BL;
+            emit(e, RK_BL, p, blo, sdir);
+        }
+    }
+    // ---- sample_environment_map (:569-631)
+    {
+        const float total = S.cdf[S.ew * S.eh - 1];
+        int x, y;
+        cdf_search(S, P.rng.next() * total, x, y, st);
+        float u = (float)x / (float)S.ew, v = (float)y / (float)S.eh;
+        float phi = (float)((double)(u * 2.0f) * 3.14159265358979323846);
+        float theta = (float)((double)v * 3.14159265358979323846);
+        float st_ = rt_sinf(theta), ct_ = rt_cosf(theta);
+        V3 dir = v3(-st_ * rt_cosf(phi), -ct_, -st_ * rt_sinf(phi));
+        float cosine = dot(h.n, dir);
+        if (cosine > 0.0f) {
+            float pdf = S.env_lum[y * S.ew + x] / total;
+            pdf = (float)((double)((pdf * (float)S.ew) * (float)S.eh) /
+                          (2.0 * 3.14159265358979323846 * 3.14159265358979323846 * (double)st_));
+            Col rad = env_texel(S, x, y, st);
+            Col brdf = ct_brdf(m, dir, neg(rd), h.n);
+            float bp = ct_pdf(m, neg(rd), dir, h.n);
+            float mis = power_heuristic(pdf, bp);
+            W.q_env[p] = f4(cdiv(cmul(cscale(cscale(brdf, cosine), mis), rad), pdf), 0.0f);
+            fl |= PF_ESH;
+            emit(e, RK_ESH, p, add(h.p, mul(1.0e-4f, h.n)), dir);
+        }
+        float bsp;
+        V3 bdir = v3(0.0f, 0.0f, 0.0f);
+        Col bis = ct_sample(m, neg(rd), h.n, bdir, bsp, P.rng);
+        cosine = rt_max(dot(h.n, bdir), 0.0f);
+        if (bsp != 0.0f && cosine > 0.0f) {
+            Col sky = env_from_dir(S, bdir, st);
+            float th = rt_acosf(bdir.z);
+            float sth = rt_sinf(th);
+            float epdf = (0.3086f * sky.r + 0.6094f * sky.g + 0.0820f * sky.b) / S.cdf[S.ew * S.eh - 1];
+            epdf *= (float)(S.ew * S.eh);
+            epdf = (float)((double)epdf / (2.0 * 3.14159265358979323846 * 3.14159265358979323846 * (double)sth));
+            float mis = power_heuristic(bsp, epdf);
+            W.q_benv[p] = f4(cdiv(cmul(cscale(cscale(sky, mis), cosine), bis), bsp), 0.0f);
+            fl |= PF_BENV;
+            emit(e, RK_BENV, p, add(h.p, mul(1.0e-5f, h.n)), bdir);
+        }
+    }
+    // ---- continuation (:123-141)
+    float bpdf;
+    V3 dir = v3(0.0f, 0.0f, 0.0f);
+    Col brdf = ct_sample(m, neg(rd), h.n, dir, bpdf, P.rng);
+    if (P.bounce == 0) {
+        fl |= PF_EMIT0;
+        W.q_em[p] = f4(m.emission, 0.0f);
+    }
+    W.q_hn[p] = f4(h.n, 0.0f);
+    W.q_thr[p] = f4(P.thr, 0.0f);
+    if ((brdf.r == 0.0f && brdf.g == 0.0f && brdf.b == 0.0f) || bpdf < 1.0e-8f || rt_isinf(bpdf)) {
+        fl |= PF_END;  // `break` after this bounce's light is added
+    } else {
+        P.thr = cmul(P.thr, cdiv(cscale(brdf, rt_max(0.0f, dot(dir, h.n))), bpdf));
+        P.ro = add(h.p, mul(1.0e-4f, h.n));
+        P.rd = dir;
+        if (P.bounce + 1 < W.bounces) {
+            P.bounce++;
+            fl |= PF_CONT;
+            emit(e, RK_CONT, p, P.ro, P.rd);
+        } else {
+            fl |= PF_END;  // the bounce loop is over
+        }
+    }
+    P.flags = fl;
+}
+
+// --------------------------------------------------------------- resolve
+// sc += (light + bmis + brdf_sample + env_sample) * thr with the
+// reference's association: lr = light + bmis, er = brdf_sample + env_sample,
+// sc = sc + (lr + er) * thr (render_kernel.cpp:113-128).
+RT_HD void resolve(const WaveView& W, int p, PathReg& P, Stats* st)
+{
+    const RtSceneView& S = W.S;
+    const uint32_t fl = P.flags;
+    Col light = col(0.0f);
+    if (fl & PF_LSH) {
+        const float4_ q = W.q_light[p];
+        const float t = W.r_lsh_t[p];
+        const bool in_shadow = t > 0.0f && t + 1.0e-4f < q.w;
+        if (!in_shadow) light = colof(q);
+    }
+    Col bmis = col(0.0f);
+    if (fl & PF_BL) {
+        const float t = W.r_bl_t[p];
+        if (t > 0.0f) {
+            const int k = W.r_bl_k[p];
+            const float4_ qb = W.q_bl[p];
+            const V3 sdir = v3of(W.q_sdir[p]);
+            const V3 hn = v3of(W.q_hn[p]);
+            Hit nh;
+            hit_from(S, v3of(W.q_blo[p]), sdir, t, k, nh);
+            float ca = rt_max(dot(nh.n, neg(sdir)), 0.0f);
+            if (ca > 0.0f) {
+                if (st) st->c[RT_STAT_MAT]++;
+                const Mat mm = load_mat(S, nh.prim);
+                const Col e = mm.emission;
+                if (e.r > 0 || e.g > 0 || e.b > 0) {
+                    float d2 = t * t;
+                    // Triangle::area (triangle.cpp:8-11) of the hit triangle; an
+                    // emissive *sphere* hit reads past the triangle buffer in the
+                    // reference (undefined behaviour): area 0 here.
+                    float la = k < 0 ? 0.0f : length(cross(ld3(S.tri4[3 * k + 1]), ld3(S.tri4[3 * k + 2]))) / 2;
+                    float lp = d2 / (la * ca);
+                    float mis = power_heuristic(qb.w, lp);
+                    float cosine = dot(hn, sdir);
+                    bmis = cdiv(cscale(cmul(cscale(colof(qb), cosine), e), mis), qb.w);
+                }
+            }
+        }
+    }
+    Col env_sample = col(0.0f), brdf_sample = col(0.0f);
+    if ((fl & PF_ESH) && !W.r_esh[p]) env_sample = colof(W.q_env[p]);
+    if ((fl & PF_BENV) && !W.r_benv[p]) brdf_sample = colof(W.q_benv[p]);
+    const Col lr = cadd(light, bmis);
+    const Col er = cadd(brdf_sample, env_sample);
+    if (fl & PF_EMIT0) P.sc = cadd(P.sc, colof(W.q_em[p]));
+    P.sc = cadd(P.sc, cmul(cadd(lr, er), colof(W.q_thr[p])));
+}
+
+// One iteration of path slot p: resolve the bounce shaded last iteration,
+// consume the continuation query, shade the new hit or end the sample,
+// start the next sample. Fills `e` with the rays for the next trace.
+RT_HD void path_step(const WaveView& W, int p, Emit& e, Stats* st)
+{
+    PathReg P;
+    load_path(W, p, P);
+    e.mask = 0;
+    e.active = true;
+    if (P.flags & PF_AUX) resolve(W, p, P, st);
+    bool end = (P.flags & PF_END) != 0;
+    if (P.flags & PF_CONT) {
+        const float t = W.r_cont_t[p];
+        Hit h;
+        if (hit_from(W.S, P.ro, P.rd, t, W.r_cont_k[p], h)) {
+            shade(W, p, P, h, e, st);
+            store_path(W, p, P);
+            return;
+        }
+        // MISSED (:143-160): the next loop iteration adds the sky only when
+        // it is bounce 1, i.e. the camera ray missed; then `break`.
+        if (P.bounce == 0 && W.bounces >= 2) P.sc = cadd(P.sc, cmul(env_from_dir(W.S, P.rd, st), P.thr));
+        end = true;
+    }
+    if (end) {
+        P.fin = cadd(P.fin, P.sc);
+        if (++P.sample == W.spp) {
+            e.active = false;
+        } else {
+            e.active = start_sample(W, p, P, e);
+        }
+        if (!e.active) finish_pixel(W, p, P);
+    }
+    store_path(W, p, P);
+}
+
+// --------------------------------------------------------------- queries
+// Closest-hit query (INTERSECT_SCENE = intersect_scene_bvh :485-502):
+// octree, then the sphere loop. Writes (t, k) with k = leaf-order triangle,
+// -2 - sphere index, or -1 for none.
+RT_HD void query_closest(const RtSceneView& S, V3 o, V3 d, StackEnt* stack, float& t, int& k, Stats* st)
+{
+    trace_closest(S, o, d, stack, t, k, st);
+    for (int i = 0; i < S.n_spheres; i++) {
+        Hit sh;
+        if (sphere_test(S.spheres, i, o, d, sh))
+            if (sh.t < t || t == -1.0f) {
+                t = sh.t;
+                k = sh.k;
+            }
+    }
+}
+
+}  // namespace rtk

@@ -229,10 +229,25 @@ class RenderKernel:
     def set_stats(self, on: bool):
         self.L.rt_set_stats(self.ctx, 1 if on else 0)
 
-    def stats(self) -> np.ndarray:
-        out = np.zeros(8, dtype=np.uint64)
-        self.L.rt_get_stats(self.ctx, ptr(out), 8)
-        return out
+    def stats(self) -> dict:
+        """Counters of the last render (rt_set_stats(True) first), by name."""
+        from ._capi import STAT_NAMES
+        out = np.zeros(len(STAT_NAMES), dtype=np.uint64)
+        self.L.rt_get_stats(self.ctx, ptr(out), len(STAT_NAMES))
+        return {k: int(v) for k, v in zip(STAT_NAMES, out)}
+
+    def kernel_timing(self, enable: int = -1):
+        """Per-kernel-class GPU time (HIP events around every launch) since
+        timing was last enabled: {class: (total_ms, launches)} for the
+        closest-hit trace, occlusion trace and step kernels. enable=1/0
+        turns timing on/off and resets the totals; -1 only reads."""
+        ms = np.zeros(3, dtype=np.float64)
+        n = np.zeros(3, dtype=np.int64)
+        check(self.L, self.L.rt_device_kernel_timing(self.ctx, enable, ptr(ms), ptr(n)), self.ctx, "kernel_timing")
+        return {k: (float(a), int(b)) for k, a, b in zip(("trace_closest", "trace_any", "step"), ms, n)}
+
+    def last_iterations(self) -> int:
+        return int(self.L.rt_device_last_iterations(self.ctx))
 
     def last_kernel_ms(self) -> float:
         return float(self.L.rt_last_kernel_ms(self.ctx))

@@ -59,9 +59,14 @@ _SIGS = {
     # product-only extras
     "rt_device_libm": (I, [I, I, P, P, P, I]),
     "rt_device_last_kernel_ms": (ctypes.c_double, [P]),
+    "rt_device_kernel_timing": (I, [P, I, P, P]),
+    "rt_device_last_iterations": (I, [P]),
     # hostsim-only extra
     "rt_hostsim_heap_order": (I, [P, I, P, P]),
 }
+
+STAT_NAMES = ["rays", "vol", "tri", "leaf", "mat", "env", "cdf", "heap_slow", "any_rays", "any_vol", "any_tri",
+              "any_leaf"]
 
 _libs: dict = {}
 

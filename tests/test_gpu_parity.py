@@ -222,3 +222,15 @@ def test_gpu_ieee_div_sqrt_f64():
     assert L.rt_device_libm(0, 9, _capi.ptr(x), _capi.ptr(y), _capi.ptr(out), x.shape[0]) == 0
     want = (x.astype(np.float64) * 0.31830988618379067154 / y.astype(np.float64)).astype(np.float32)
     np.testing.assert_array_equal(out.view(np.uint32), want.view(np.uint32))
+
+
+def test_gpu_slab_division_exact():
+    """The slab quotient (float)((double)a * (1.0/(double)den)) on gfx950 ==
+    IEEE f32 a/den (the reference's division, bounding_volume.h:113-114)."""
+    from test_numerics import division_cases
+    a, d = division_cases(400000)
+    out = np.zeros_like(a)
+    assert _capi.lib().rt_device_libm(0, 10, _capi.ptr(a), _capi.ptr(d), _capi.ptr(out), a.shape[0]) == 0
+    want = (a / d).astype(np.float32)
+    same = (out.view(np.uint32) == want.view(np.uint32)) | (np.isnan(out) & np.isnan(want))
+    assert same.all(), (a[~same][:4], d[~same][:4])
