@@ -14,6 +14,12 @@
 #include "rt_context.h"
 #include "rt_wave.h"
 
+// Short-stack capacity of the host build: smaller than the device's so that
+// the CPU tests take the overflow fallback often (dragon rays need up to 19).
+#ifndef RT_HOSTSIM_SHORT_CAP
+#define RT_HOSTSIM_SHORT_CAP 8
+#endif
+
 int rt_backend_create(rt_context*) { return RT_OK; }
 void rt_backend_destroy(rt_context*) {}
 int rt_backend_upload(rt_context*) { return RT_OK; }
@@ -75,6 +81,7 @@ static int run_wave_host(rt_context* c, int w, int h, int spp, int bounces, cons
         {
             std::vector<rtk::StackEnt> stack(RT_STACK_CAP);
             std::vector<uint32_t> astack(RT_STACK_CAP);
+            rtk::ArrayStack<RT_HOSTSIM_SHORT_CAP> sstack;
             rtk::Stats* ps = c->stats_enabled ? &st[omp_get_thread_num()] : nullptr;
 #pragma omp for schedule(dynamic, 64)
             for (int idx = 0; idx < nc; idx++) {
@@ -91,7 +98,9 @@ static int run_wave_host(rt_context* c, int w, int h, int spp, int bounces, cons
                 const int slot = (int)rt_asuint(r.o.w);
                 float t;
                 int k;
-                rtk::query_closest(W.S, rtk::v3of(r.o), rtk::v3of(r.d), stack.data(), t, k, ps);
+                // a small short stack so the tests exercise the overflow fallback
+                if (!rtk::query_closest_short(W.S, rtk::v3of(r.o), rtk::v3of(r.d), sstack, t, k, ps))
+                    rtk::query_closest(W.S, rtk::v3of(r.o), rtk::v3of(r.d), stack.data(), t, k, ps);
                 if (kind == rtk::RK_CONT) {
                     W.r_cont_t[slot] = t;
                     W.r_cont_k[slot] = k;
@@ -110,7 +119,8 @@ static int run_wave_host(rt_context* c, int w, int h, int spp, int bounces, cons
                 const int slot = (int)rt_asuint(r.o.w);
                 bool hit;
                 if (W.any_rays) {
-                    hit = rtk::trace_any(W.S, rtk::v3of(r.o), rtk::v3of(r.d), astack.data(), ps);
+                    const int a = rtk::trace_any_short(W.S, rtk::v3of(r.o), rtk::v3of(r.d), sstack, ps);
+                    hit = a >= 0 ? a == 1 : rtk::trace_any(W.S, rtk::v3of(r.o), rtk::v3of(r.d), astack.data(), ps);
                 } else {
                     float t;
                     int k;

@@ -44,6 +44,8 @@ enum {
     C_TK_CLOSEST = rtk::RK_COUNT,
     C_TK_ANY,
     C_TK_STEP,
+    C_OVF_CLOSEST,            // rays whose short stack overflowed (re-traced by the fallback kernels)
+    C_OVF_ANY,
     C_ACT0,                   // live-slot counts, double-buffered
     C_ACT1,
     C_COUNT
@@ -107,6 +109,25 @@ __device__ __forceinline__ int wave_append(int32_t* counter, bool want)
     const unsigned long long lt = (lane_id() == 0) ? 0ull : (b & (~0ull >> (64 - lane_id())));
     return want ? base + __popcll(lt) : -1;
 }
+
+// Per-lane traversal stack in LDS: entry i of thread t at [i * 256 + t]
+// (a wave at equal depth touches 64 consecutive words: no bank conflicts).
+template <int N>
+struct LdsStack {
+    static constexpr int CAP = N;
+    uint32_t* r;
+    float* k;
+    __device__ __forceinline__ uint32_t rec(int i) const { return r[i * 256]; }
+    __device__ __forceinline__ float key(int i) const { return k[i * 256]; }
+    __device__ __forceinline__ void set(int i, uint32_t rv, float kv)
+    {
+        r[i * 256] = rv;
+        k[i * 256] = kv;
+    }
+    __device__ __forceinline__ void set_rec(int i, uint32_t rv) { r[i * 256] = rv; }
+};
+#define RT_LDS_CAP_CLOSEST 16
+#define RT_LDS_CAP_ANY 24
 
 // One ticket of 64 work items per wave.
 __device__ __forceinline__ int wave_ticket(int32_t* ticket)
@@ -175,13 +196,40 @@ __global__ __launch_bounds__(256) void k_step(rtk::WaveView W, const int32_t* ac
     flush_stats<STATS>(st, stats);
 }
 
-template <bool STATS>
-__global__ __launch_bounds__(256) void k_trace_closest(rtk::WaveView W, unsigned long long* stats)
+// Decodes a closest-hit work index into (kind, queue position).
+__device__ __forceinline__ int closest_kind(const rtk::WaveView& W, int& i)
 {
-    const int n0 = W.counters[C_Q0 + rtk::RK_CONT], n1 = W.counters[C_Q0 + rtk::RK_LSH],
-              n2 = W.counters[C_Q0 + rtk::RK_BL];
-    const int total = n0 + n1 + n2;
-    rtk::StackEnt stack[RT_STACK_CAP];
+    const int n0 = W.counters[C_Q0 + rtk::RK_CONT], n1 = W.counters[C_Q0 + rtk::RK_LSH];
+    if (i < n0) return rtk::RK_CONT;
+    i -= n0;
+    if (i < n1) return rtk::RK_LSH;
+    i -= n1;
+    return rtk::RK_BL;
+}
+
+__device__ __forceinline__ void store_closest(const rtk::WaveView& W, int kind, int slot, float t, int k)
+{
+    if (kind == rtk::RK_CONT) {
+        W.r_cont_t[slot] = t;
+        W.r_cont_k[slot] = k;
+    } else if (kind == rtk::RK_LSH) {
+        W.r_lsh_t[slot] = t;
+    } else {
+        W.r_bl_t[slot] = t;
+        W.r_bl_k[slot] = k;
+    }
+}
+
+// Closest-hit queries with the LDS short stack; overflowing rays go to the
+// fallback queue (k_trace_closest_ovf, unbounded scratch stack).
+template <bool STATS>
+__global__ __launch_bounds__(256, 5) void k_trace_closest(rtk::WaveView W, int32_t* ovf, unsigned long long* stats)
+{
+    __shared__ uint32_t s_r[RT_LDS_CAP_CLOSEST * 256];
+    __shared__ float s_k[RT_LDS_CAP_CLOSEST * 256];
+    LdsStack<RT_LDS_CAP_CLOSEST> stk{s_r + threadIdx.x, s_k + threadIdx.x};
+    const int total = W.counters[C_Q0 + rtk::RK_CONT] + W.counters[C_Q0 + rtk::RK_LSH] +
+                      W.counters[C_Q0 + rtk::RK_BL];
     rtk::Stats st;
     if (STATS)
         for (int i = 0; i < RT_STAT_COUNT; i++) st.c[i] = 0;
@@ -189,41 +237,55 @@ __global__ __launch_bounds__(256) void k_trace_closest(rtk::WaveView W, unsigned
         const int base = wave_ticket(W.counters + C_TK_CLOSEST);
         if (base >= total) break;
         const int idx = base + lane_id();
+        bool over = false;
         if (idx < total) {
-            int kind = rtk::RK_CONT, i = idx;
-            if (i >= n0) {
-                i -= n0;
-                kind = rtk::RK_LSH;
-                if (i >= n1) {
-                    i -= n1;
-                    kind = rtk::RK_BL;
-                }
-            }
+            int i = idx;
+            const int kind = closest_kind(W, i);
             const rtk::RayRec r = W.q[kind][i];
-            const int slot = (int)rt_asuint(r.o.w);
             float t;
             int k;
-            rtk::query_closest(W.S, rtk::v3of(r.o), rtk::v3of(r.d), stack, t, k, STATS ? &st : nullptr);
-            if (kind == rtk::RK_CONT) {
-                W.r_cont_t[slot] = t;
-                W.r_cont_k[slot] = k;
-            } else if (kind == rtk::RK_LSH) {
-                W.r_lsh_t[slot] = t;
-            } else {
-                W.r_bl_t[slot] = t;
-                W.r_bl_k[slot] = k;
-            }
+            if (rtk::query_closest_short(W.S, rtk::v3of(r.o), rtk::v3of(r.d), stk, t, k, STATS ? &st : nullptr))
+                store_closest(W, kind, (int)rt_asuint(r.o.w), t, k);
+            else
+                over = true;
         }
+        const int o = wave_append(W.counters + C_OVF_CLOSEST, over);
+        if (over) ovf[o] = idx;
     }
     flush_stats<STATS>(st, stats);
 }
 
-template <bool STATS, bool ANY>
-__global__ __launch_bounds__(256) void k_trace_any(rtk::WaveView W, unsigned long long* stats)
+template <bool STATS>
+__global__ __launch_bounds__(256) void k_trace_closest_ovf(rtk::WaveView W, const int32_t* ovf,
+                                                           unsigned long long* stats)
 {
+    const int n = W.counters[C_OVF_CLOSEST];
+    rtk::StackEnt stack[RT_STACK_CAP];
+    rtk::Stats st;
+    if (STATS)
+        for (int i = 0; i < RT_STAT_COUNT; i++) st.c[i] = 0;
+    for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += gridDim.x * blockDim.x) {
+        int i = ovf[j];
+        const int kind = closest_kind(W, i);
+        const rtk::RayRec r = W.q[kind][i];
+        float t;
+        int k;
+        rtk::query_closest(W.S, rtk::v3of(r.o), rtk::v3of(r.d), stack, t, k, STATS ? &st : nullptr);
+        store_closest(W, kind, (int)rt_asuint(r.o.w), t, k);
+    }
+    flush_stats<STATS>(st, stats);
+}
+
+// Occlusion queries. ANY: the any-hit walk with an LDS short stack
+// (overflow -> k_trace_any_ovf); !ANY (analytic spheres present): the exact
+// closest-hit logic with an unbounded stack.
+template <bool STATS, bool ANY>
+__global__ __launch_bounds__(256) void k_trace_any(rtk::WaveView W, int32_t* ovf, unsigned long long* stats)
+{
+    __shared__ uint32_t s_r[ANY ? RT_LDS_CAP_ANY * 256 : 1];
+    LdsStack<RT_LDS_CAP_ANY> stk{s_r + (ANY ? threadIdx.x : 0), nullptr};
     const int n0 = W.counters[C_Q0 + rtk::RK_ESH], n1 = W.counters[C_Q0 + rtk::RK_BENV];
     const int total = n0 + n1;
-    uint32_t stack[ANY ? RT_STACK_CAP : 1];
     rtk::StackEnt cstack[ANY ? 1 : RT_STACK_CAP];
     rtk::Stats st;
     if (STATS)
@@ -232,21 +294,46 @@ __global__ __launch_bounds__(256) void k_trace_any(rtk::WaveView W, unsigned lon
         const int base = wave_ticket(W.counters + C_TK_ANY);
         if (base >= total) break;
         const int idx = base + lane_id();
+        bool over = false;
         if (idx < total) {
             const int kind = idx < n0 ? rtk::RK_ESH : rtk::RK_BENV;
             const rtk::RayRec r = W.q[kind][idx < n0 ? idx : idx - n0];
             const int slot = (int)rt_asuint(r.o.w);
-            bool hit;
+            int hit;
             if (ANY) {
-                hit = rtk::trace_any(W.S, rtk::v3of(r.o), rtk::v3of(r.d), stack, STATS ? &st : nullptr);
-            } else {  // analytic spheres present: the reference's exact closest-hit logic
+                hit = rtk::trace_any_short(W.S, rtk::v3of(r.o), rtk::v3of(r.d), stk, STATS ? &st : nullptr);
+            } else {
                 float t;
                 int k;
                 rtk::query_closest(W.S, rtk::v3of(r.o), rtk::v3of(r.d), cstack, t, k, STATS ? &st : nullptr);
-                hit = t > 0.0f;
+                hit = t > 0.0f ? 1 : 0;
             }
-            (kind == rtk::RK_ESH ? W.r_esh : W.r_benv)[slot] = hit ? 1 : 0;
+            if (hit >= 0)
+                (kind == rtk::RK_ESH ? W.r_esh : W.r_benv)[slot] = (uint8_t)hit;
+            else
+                over = true;
         }
+        const int o = wave_append(W.counters + C_OVF_ANY, over);
+        if (over) ovf[o] = idx;
+    }
+    flush_stats<STATS>(st, stats);
+}
+
+template <bool STATS>
+__global__ __launch_bounds__(256) void k_trace_any_ovf(rtk::WaveView W, const int32_t* ovf, unsigned long long* stats)
+{
+    const int n = W.counters[C_OVF_ANY];
+    const int n0 = W.counters[C_Q0 + rtk::RK_ESH];
+    uint32_t stack[RT_STACK_CAP];
+    rtk::Stats st;
+    if (STATS)
+        for (int i = 0; i < RT_STAT_COUNT; i++) st.c[i] = 0;
+    for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += gridDim.x * blockDim.x) {
+        const int idx = ovf[j];
+        const int kind = idx < n0 ? rtk::RK_ESH : rtk::RK_BENV;
+        const rtk::RayRec r = W.q[kind][idx < n0 ? idx : idx - n0];
+        const bool hit = rtk::trace_any(W.S, rtk::v3of(r.o), rtk::v3of(r.d), stack, STATS ? &st : nullptr);
+        (kind == rtk::RK_ESH ? W.r_esh : W.r_benv)[(int)rt_asuint(r.o.w)] = hit ? 1 : 0;
     }
     flush_stats<STATS>(st, stats);
 }
@@ -422,6 +509,9 @@ static int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounce
     const int step_blocks = std::min((n + threads - 1) / threads, dev_cus * 8);
     const int trace_blocks = std::min((3 * n + threads - 1) / threads, dev_cus * 8);
     const int any_blocks = std::min((2 * n + threads - 1) / threads, dev_cus * 8);
+    const int ovf_blocks = dev_cus;
+    int32_t* ovf_c = W.ovf_closest;
+    int32_t* ovf_a = W.ovf_any;
     // each sample takes at most bounces + 1 iterations; +2 for init / final resolve
     long max_iters = (long)spp * ((long)bounces + 1) + 2;
     if (b->timing) {
@@ -435,19 +525,28 @@ static int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounce
         const int cur = it & 1;
         const bool T = b->timing;
         if (T) HIPCHK(c, hipEventRecord(b->tev[0][it], s));
-        if (S)
-            hipLaunchKernelGGL(k_trace_closest<true>, dim3(trace_blocks), dim3(threads), 0, s, W, stats);
-        else
-            hipLaunchKernelGGL(k_trace_closest<false>, dim3(trace_blocks), dim3(threads), 0, s, W, stats);
+        if (S) {
+            hipLaunchKernelGGL(k_trace_closest<true>, dim3(trace_blocks), dim3(threads), 0, s, W, ovf_c, stats);
+            hipLaunchKernelGGL(k_trace_closest_ovf<true>, dim3(ovf_blocks), dim3(threads), 0, s, W, ovf_c, stats);
+        } else {
+            hipLaunchKernelGGL(k_trace_closest<false>, dim3(trace_blocks), dim3(threads), 0, s, W, ovf_c, stats);
+            hipLaunchKernelGGL(k_trace_closest_ovf<false>, dim3(ovf_blocks), dim3(threads), 0, s, W, ovf_c, stats);
+        }
         if (T) HIPCHK(c, hipEventRecord(b->tev[1][it], s));
         if (S && W.any_rays)
-            hipLaunchKernelGGL((k_trace_any<true, true>), dim3(any_blocks), dim3(threads), 0, s, W, stats);
+            hipLaunchKernelGGL((k_trace_any<true, true>), dim3(any_blocks), dim3(threads), 0, s, W, ovf_a, stats);
         else if (S)
-            hipLaunchKernelGGL((k_trace_any<true, false>), dim3(any_blocks), dim3(threads), 0, s, W, stats);
+            hipLaunchKernelGGL((k_trace_any<true, false>), dim3(any_blocks), dim3(threads), 0, s, W, ovf_a, stats);
         else if (W.any_rays)
-            hipLaunchKernelGGL((k_trace_any<false, true>), dim3(any_blocks), dim3(threads), 0, s, W, stats);
+            hipLaunchKernelGGL((k_trace_any<false, true>), dim3(any_blocks), dim3(threads), 0, s, W, ovf_a, stats);
         else
-            hipLaunchKernelGGL((k_trace_any<false, false>), dim3(any_blocks), dim3(threads), 0, s, W, stats);
+            hipLaunchKernelGGL((k_trace_any<false, false>), dim3(any_blocks), dim3(threads), 0, s, W, ovf_a, stats);
+        if (W.any_rays) {
+            if (S)
+                hipLaunchKernelGGL(k_trace_any_ovf<true>, dim3(ovf_blocks), dim3(threads), 0, s, W, ovf_a, stats);
+            else
+                hipLaunchKernelGGL(k_trace_any_ovf<false>, dim3(ovf_blocks), dim3(threads), 0, s, W, ovf_a, stats);
+        }
         if (T) HIPCHK(c, hipEventRecord(b->tev[2][it], s));
         hipLaunchKernelGGL(k_reset, dim3(1), dim3(64), 0, s, cnt, C_ACT0 + (cur ^ 1));
         // step: reads the list written last iteration (lists[cur]) -> lists[cur ^ 1]

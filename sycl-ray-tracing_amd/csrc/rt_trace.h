@@ -346,6 +346,170 @@ RT_HD void trace_closest(const RtSceneView& S, V3 o, V3 d, StackEnt* stack, floa
     }
 }
 
+// ------------------------------------------- short-stack closest-hit walk
+// The same traversal as trace_closest() with a bounded stack of 8-byte
+// entries (record | FIRST | LAST, t_near) that the gfx950 kernel keeps in
+// LDS. Two changes of representation, no change of order or result:
+//  * "the previous sibling returned true" needs "a leaf was visited since
+//    that sibling was popped": one bit per stack group level in `lmask`,
+//    cleared when a non-last entry of the level is popped, set (all levels)
+//    on every leaf visit — instead of a leaf-count snapshot per entry;
+//  * equal-key children are ordered by running std::push_heap / pop_heap in
+//    place over their stack slots: pop_heap leaves the popped element at the
+//    end of the range, so after m pops slot sp+m-1 holds the first popped
+//    (nearest) child — exactly the push layout (nearest on top).
+// Returns false if the stack would overflow (the caller re-traces the ray
+// with trace_closest()); best_t / best_k are then meaningless.
+template <class STK>
+RT_HD void stk_sift_up(STK& s, int base, int hole, float key, uint32_t val)
+{
+    int parent = (hole - 1) / 2;
+    while (hole > 0 && s.key(base + parent) > key) {
+        s.set(base + hole, s.rec(base + parent), s.key(base + parent));
+        hole = parent;
+        parent = (hole - 1) / 2;
+    }
+    s.set(base + hole, val, key);
+}
+
+template <class STK>
+RT_HD void stk_pop_heap(STK& s, int base, int len)  // std::pop_heap on [base, base+len)
+{
+    if (len <= 1) return;
+    const int L = len - 1;
+    const float key = s.key(base + L);
+    const uint32_t val = s.rec(base + L);
+    s.set(base + L, s.rec(base), s.key(base));
+    int hole = 0, second = 0;
+    while (second < (L - 1) / 2) {
+        second = 2 * (second + 1);
+        if (s.key(base + second) > s.key(base + second - 1)) second--;
+        s.set(base + hole, s.rec(base + second), s.key(base + second));
+        hole = second;
+    }
+    if ((L & 1) == 0 && second == (L - 2) / 2) {
+        second = 2 * (second + 1);
+        s.set(base + hole, s.rec(base + second - 1), s.key(base + second - 1));
+        hole = second - 1;
+    }
+    stk_sift_up(s, base, hole, key, val);
+}
+
+template <class STK>
+RT_HD bool trace_closest_short(const RtSceneView& S, V3 o, V3 d, STK& stk, float& best_t, int& best_k, Stats* st)
+{
+    best_t = -1.0f;
+    best_k = -1;
+    RayK K;
+    if (st) st->c[RT_STAT_RAYS]++;
+    if (!ray_setup(o, d, K)) return true;
+    const RtNode root = S.nodes[0];
+    float tn;
+    if (st) st->c[RT_STAT_VOL]++;
+    if (!slab_test(root, K, tn)) return true;
+    if (root.cnt & RT_LEAF_BIT) {
+        leaf_test(S, root, o, d, best_t, best_k, st);
+        return true;
+    }
+    int sp = 0, groups = 0;
+    uint32_t lmask = 0;
+    uint32_t base = root.ref, nc = root.cnt;
+    for (;;) {
+        // ---- expand an internal node: test its children, order, push
+        {
+            float hk[8];
+            uint32_t hi[8];
+            int m = 0;
+            bool tie = false;
+            for (uint32_t c = 0; c < nc; c++) {
+                const RtNode& ch = S.nodes[base + c];
+                float t;
+                if (slab_test(ch, K, t)) {
+#pragma unroll
+                    for (int j = 0; j < 8; j++) {
+                        tie |= (j < m) && hk[j] == t;
+                        if (j == m) {
+                            hk[j] = t;
+                            hi[j] = base + c;
+                        }
+                    }
+                    m++;
+                }
+            }
+            if (st) st->c[RT_STAT_VOL] += nc;
+            if (m > 0) {
+                if (sp + m > STK::CAP) return false;
+                if (!tie) {
+                    // distinct keys: pop order is ascending t_near; slot of rank r is sp+m-1-r
+#pragma unroll
+                    for (int i = 0; i < 8; i++) {
+                        if (i < m) {
+                            int r = 0;
+#pragma unroll
+                            for (int j = 0; j < 8; j++) r += (j < m) && hk[j] < hk[i];
+                            stk.set(sp + m - 1 - r, hi[i], hk[i]);
+                        }
+                    }
+                } else {
+                    if (st) st->c[RT_STAT_HEAP_SLOW]++;
+#pragma unroll
+                    for (int i = 0; i < 8; i++)
+                        if (i < m) stk_sift_up(stk, sp, i, hk[i], hi[i]);
+                    for (int len = m; len > 1; len--) stk_pop_heap(stk, sp, len);
+                }
+                stk.set_rec(sp + m - 1, stk.rec(sp + m - 1) | RT_ENT_FIRST);
+                stk.set_rec(sp, stk.rec(sp) | RT_ENT_LAST);
+                sp += m;
+                groups++;
+            }
+        }
+        // ---- pop the next node to visit
+        for (;;) {
+            if (sp == 0) return true;
+            --sp;
+            const uint32_t er = stk.rec(sp);
+            const uint32_t lvl = (uint32_t)(groups - 1);
+            if (!(er & RT_ENT_FIRST)) {
+                const bool prev_true = best_t > 0.0f && ((lmask >> lvl) & 1u);
+                const float closest = rt_min(100000000.0f, best_t);
+                if (prev_true && closest < stk.key(sp)) {
+                    // early exit of the parent: drop this entry and its remaining siblings
+                    if (!(er & RT_ENT_LAST))
+                        while (!(stk.rec(--sp) & RT_ENT_LAST)) {
+                        }
+                    groups--;
+                    continue;
+                }
+            }
+            if (er & RT_ENT_LAST)
+                groups--;
+            else
+                lmask &= ~(1u << lvl);
+            const RtNode& nd = S.nodes[er & RT_ENT_MASK];
+            if (nd.cnt & RT_LEAF_BIT) {
+                leaf_test(S, nd, o, d, best_t, best_k, st);
+                lmask = ~0u;
+                continue;
+            }
+            base = nd.ref;
+            nc = nd.cnt;
+            break;
+        }
+    }
+}
+
+// Plain-array stack for the host build and the scratch fallback.
+template <int N>
+struct ArrayStack {
+    static constexpr int CAP = N;
+    uint32_t r[N];
+    float k[N];
+    RT_HD uint32_t rec(int i) const { return r[i]; }
+    RT_HD float key(int i) const { return k[i]; }
+    RT_HD void set(int i, uint32_t rv, float kv) { r[i] = rv, k[i] = kv; }
+    RT_HD void set_rec(int i, uint32_t rv) { r[i] = rv; }
+};
+
 // Occlusion query: does the reference's traversal find ANY triangle hit?
 // Pruning in BVH::intersect is by slab tests (independent of the hit state)
 // and by the early exit, which only fires once a hit exists; so the
@@ -383,6 +547,45 @@ RT_HD bool trace_any(const RtSceneView& S, V3 o, V3 d, uint32_t* stack, Stats* s
         }
     }
     return false;
+}
+
+// trace_any() with a bounded stack: 1 hit, 0 no hit, -1 overflow (the
+// caller re-runs trace_any() with an unbounded stack).
+template <class STK>
+RT_HD int trace_any_short(const RtSceneView& S, V3 o, V3 d, STK& stk, Stats* st)
+{
+    RayK K;
+    if (st) st->c[RT_STAT_ANY_RAYS]++;
+    if (!ray_setup(o, d, K)) return 0;
+    float tn;
+    if (st) st->c[RT_STAT_ANY_VOL]++;
+    if (!slab_test(S.nodes[0], K, tn)) return 0;
+    int sp = 0;
+    stk.set_rec(sp++, 0);
+    while (sp > 0) {
+        const RtNode& nd = S.nodes[stk.rec(--sp)];
+        if (nd.cnt & RT_LEAF_BIT) {
+            const int n = (int)(nd.cnt & ~RT_LEAF_BIT);
+            if (st) {
+                st->c[RT_STAT_ANY_TRI] += n;
+                st->c[RT_STAT_ANY_LEAF] += 1;
+            }
+            for (int j = 0; j < n; j++) {
+                float t;
+                if (tri_test(S.tri4, (int)nd.ref + j, o, d, t)) return 1;
+            }
+            continue;
+        }
+        const int base = (int)nd.ref, nc = (int)nd.cnt;
+        if (st) st->c[RT_STAT_ANY_VOL] += nc;
+        for (int c = nc - 1; c >= 0; c--) {
+            if (slab_test(S.nodes[base + c], K, tn)) {
+                if (sp == STK::CAP) return -1;
+                stk.set_rec(sp++, (uint32_t)(base + c));
+            }
+        }
+    }
+    return 0;
 }
 
 // Sphere::intersect (sphere.h:11-52)

@@ -96,7 +96,9 @@ struct WaveView {
     uint8_t* r_benv;
     // queues
     RayRec* q[RK_COUNT];    // [n_slots] each
-    int32_t* counters;      // [RK_COUNT] queue sizes, [RK_COUNT] = next active count
+    int32_t* counters;      // queue sizes, tickets, live counts (rt_render.hip C_*)
+    int32_t* ovf_closest;   // [3 n_slots] closest-hit work items whose short stack overflowed
+    int32_t* ovf_any;       // [2 n_slots] occlusion work items whose short stack overflowed
     const int32_t* act_in;  // active slots this iteration
     int32_t* act_out;
     int n_act_in;
@@ -136,6 +138,8 @@ inline size_t wave_carve(char* base, size_t n, WaveView& W)
     for (int k = 0; k < RK_COUNT; k++) W.q[k] = (RayRec*)take(n * sizeof(RayRec));
     W.act_in = (const int32_t*)take(n * 4);
     W.act_out = (int32_t*)take(n * 4);
+    W.ovf_closest = (int32_t*)take(3 * n * 4);
+    W.ovf_any = (int32_t*)take(2 * n * 4);
     return o;
 }
 
@@ -529,9 +533,8 @@ RT_HD void path_step(const WaveView& W, int p, Emit& e, Stats* st)
 // Closest-hit query (INTERSECT_SCENE = intersect_scene_bvh :485-502):
 // octree, then the sphere loop. Writes (t, k) with k = leaf-order triangle,
 // -2 - sphere index, or -1 for none.
-RT_HD void query_closest(const RtSceneView& S, V3 o, V3 d, StackEnt* stack, float& t, int& k, Stats* st)
+RT_HD void spheres_closest(const RtSceneView& S, V3 o, V3 d, float& t, int& k)
 {
-    trace_closest(S, o, d, stack, t, k, st);
     for (int i = 0; i < S.n_spheres; i++) {
         Hit sh;
         if (sphere_test(S.spheres, i, o, d, sh))
@@ -540,6 +543,21 @@ RT_HD void query_closest(const RtSceneView& S, V3 o, V3 d, StackEnt* stack, floa
                 k = sh.k;
             }
     }
+}
+
+RT_HD void query_closest(const RtSceneView& S, V3 o, V3 d, StackEnt* stack, float& t, int& k, Stats* st)
+{
+    trace_closest(S, o, d, stack, t, k, st);
+    spheres_closest(S, o, d, t, k);
+}
+
+// Short-stack form; false = stack overflow, re-run query_closest().
+template <class STK>
+RT_HD bool query_closest_short(const RtSceneView& S, V3 o, V3 d, STK& stk, float& t, int& k, Stats* st)
+{
+    if (!trace_closest_short(S, o, d, stk, t, k, st)) return false;
+    spheres_closest(S, o, d, t, k);
+    return true;
 }
 
 }  // namespace rtk
