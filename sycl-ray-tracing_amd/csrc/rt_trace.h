@@ -128,28 +128,67 @@ RT_HD bool ray_setup(V3 o, V3 d, RayK& k)
     return !bad;
 }
 
-// BoundingVolume::intersect (bounding_volume.h:101-126). The early
-// `t_far < t_near` exit inside the loop cannot change the outcome (prefix
-// max/min are monotone), so the slab loop runs to completion.
-RT_HD bool slab_test(const RtNode& nd, const RayK& k, float& tnear)
+// A node record in registers: loaded with four 16-B loads up front (one
+// memory round trip instead of one per plane).
+struct uint2_ {
+    uint32_t x, y;
+};
+// (ref, cnt) of a record: the last 8 bytes, one load.
+RT_HD uint2_ load_link(const RtNode* nodes, uint32_t i)
+{
+    const uint2_* p = (const uint2_*)(nodes + i) + 7;
+    return *p;
+}
+
+struct NodeR {
+    float dn[7], df[7];
+    uint32_t ref, cnt;
+};
+RT_HD NodeR load_node(const RtNode* nodes, uint32_t i)
+{
+    const float4_* p = (const float4_*)(nodes + i);
+    const float4_ a = p[0], b = p[1], c = p[2], d = p[3];
+    NodeR n;
+    n.dn[0] = a.x, n.dn[1] = a.y, n.dn[2] = a.z, n.dn[3] = a.w;
+    n.dn[4] = b.x, n.dn[5] = b.y, n.dn[6] = b.z, n.df[0] = b.w;
+    n.df[1] = c.x, n.df[2] = c.y, n.df[3] = c.z, n.df[4] = c.w;
+    n.df[5] = d.x, n.df[6] = d.y;
+    n.ref = rt_asuint(d.z);
+    n.cnt = rt_asuint(d.w);
+    return n;
+}
+
+// BoundingVolume::intersect (bounding_volume.h:101-126), branch-free:
+//  * a plane with denom == 0 is skipped by the reference; here it yields
+//    (-inf, +inf), the identity of the max / min that follow;
+//  * `if (denom < 0) swap(near, far)` is applied to the operands instead of
+//    the quotients (same two quotients, same arithmetic);
+//  * the early `t_far < t_near` exit cannot change the outcome (prefix
+//    max/min are monotone), so all planes are evaluated.
+RT_HD bool slab_test(const NodeR& nd, const RayK& k, float& tnear)
 {
     float tn = -__builtin_inff(), tf = __builtin_inff();
 #pragma unroll
     for (int i = 0; i < 7; i++) {
         const float d = k.den[i];
-        if (d == 0.0f) continue;
-        float a = slab_div(nd.dn[i] - k.num[i], k.rinv[i]);
-        float b = slab_div(nd.df[i] - k.num[i], k.rinv[i]);
-        if (d < 0.0f) {
-            float t = a;
-            a = b;
-            b = t;
+        const bool neg = d < 0.0f;
+        float a = slab_div((neg ? nd.df[i] : nd.dn[i]) - k.num[i], k.rinv[i]);
+        float b = slab_div((neg ? nd.dn[i] : nd.df[i]) - k.num[i], k.rinv[i]);
+        if (d == 0.0f) {
+            a = -__builtin_inff();
+            b = __builtin_inff();
         }
         tn = rt_max(tn, a);
         tf = rt_min(tf, b);
     }
     tnear = tn;
     return !(tf < tn);
+}
+RT_HD bool slab_test(const RtNode& nd, const RayK& k, float& tnear)
+{
+    NodeR r;
+    for (int i = 0; i < 7; i++) r.dn[i] = nd.dn[i], r.df[i] = nd.df[i];
+    return slab_test(r, k, tnear);
 }
 
 // Triangle::intersect (triangle.h:16-60) on the pre-subtracted record.
@@ -229,10 +268,11 @@ RT_HD void heap_order(float* key, int* id, int m, float* okey, int* oid)
     }
 }
 
-RT_HD void leaf_test(const RtSceneView& S, const RtNode& nd, V3 o, V3 d, float& best_t, int& best_k, Stats* st)
+RT_HD void leaf_test(const RtSceneView& S, uint32_t ref, uint32_t cnt, V3 o, V3 d, float& best_t, int& best_k,
+                     Stats* st)
 {
-    const int n = (int)(nd.cnt & ~RT_LEAF_BIT);
-    const int k0 = (int)nd.ref;
+    const int n = (int)(cnt & ~RT_LEAF_BIT);
+    const int k0 = (int)ref;
     for (int j = 0; j < n; j++) {
         float t;
         if (tri_test(S.tri4, k0 + j, o, d, t))
@@ -262,7 +302,7 @@ RT_HD void trace_closest(const RtSceneView& S, V3 o, V3 d, StackEnt* stack, floa
     if (st) st->c[RT_STAT_VOL]++;
     if (!slab_test(root, K, tn)) return;
     if (root.cnt & RT_LEAF_BIT) {
-        leaf_test(S, root, o, d, best_t, best_k, st);
+        leaf_test(S, root.ref, root.cnt, o, d, best_t, best_k, st);
         return;
     }
     int sp = 0;
@@ -337,7 +377,7 @@ RT_HD void trace_closest(const RtSceneView& S, V3 o, V3 d, StackEnt* stack, floa
             rec = e.rec & RT_ENT_MASK;
             nd = S.nodes[rec];
             if (nd.cnt & RT_LEAF_BIT) {
-                leaf_test(S, nd, o, d, best_t, best_k, st);
+                leaf_test(S, nd.ref, nd.cnt, o, d, best_t, best_k, st);
                 leaves++;
                 continue;
             }
@@ -408,7 +448,7 @@ RT_HD bool trace_closest_short(const RtSceneView& S, V3 o, V3 d, STK& stk, float
     if (st) st->c[RT_STAT_VOL]++;
     if (!slab_test(root, K, tn)) return true;
     if (root.cnt & RT_LEAF_BIT) {
-        leaf_test(S, root, o, d, best_t, best_k, st);
+        leaf_test(S, root.ref, root.cnt, o, d, best_t, best_k, st);
         return true;
     }
     int sp = 0, groups = 0;
@@ -422,7 +462,7 @@ RT_HD bool trace_closest_short(const RtSceneView& S, V3 o, V3 d, STK& stk, float
             int m = 0;
             bool tie = false;
             for (uint32_t c = 0; c < nc; c++) {
-                const RtNode& ch = S.nodes[base + c];
+                const NodeR ch = load_node(S.nodes, base + c);
                 float t;
                 if (slab_test(ch, K, t)) {
 #pragma unroll
@@ -485,14 +525,14 @@ RT_HD bool trace_closest_short(const RtSceneView& S, V3 o, V3 d, STK& stk, float
                 groups--;
             else
                 lmask &= ~(1u << lvl);
-            const RtNode& nd = S.nodes[er & RT_ENT_MASK];
-            if (nd.cnt & RT_LEAF_BIT) {
-                leaf_test(S, nd, o, d, best_t, best_k, st);
+            const uint2_ link = load_link(S.nodes, er & RT_ENT_MASK);
+            if (link.y & RT_LEAF_BIT) {
+                leaf_test(S, link.x, link.y, o, d, best_t, best_k, st);
                 lmask = ~0u;
                 continue;
             }
-            base = nd.ref;
-            nc = nd.cnt;
+            base = link.x;
+            nc = link.y;
             break;
         }
     }
@@ -563,23 +603,23 @@ RT_HD int trace_any_short(const RtSceneView& S, V3 o, V3 d, STK& stk, Stats* st)
     int sp = 0;
     stk.set_rec(sp++, 0);
     while (sp > 0) {
-        const RtNode& nd = S.nodes[stk.rec(--sp)];
-        if (nd.cnt & RT_LEAF_BIT) {
-            const int n = (int)(nd.cnt & ~RT_LEAF_BIT);
+        const uint2_ link = load_link(S.nodes, stk.rec(--sp));
+        if (link.y & RT_LEAF_BIT) {
+            const int n = (int)(link.y & ~RT_LEAF_BIT);
             if (st) {
                 st->c[RT_STAT_ANY_TRI] += n;
                 st->c[RT_STAT_ANY_LEAF] += 1;
             }
             for (int j = 0; j < n; j++) {
                 float t;
-                if (tri_test(S.tri4, (int)nd.ref + j, o, d, t)) return 1;
+                if (tri_test(S.tri4, (int)link.x + j, o, d, t)) return 1;
             }
             continue;
         }
-        const int base = (int)nd.ref, nc = (int)nd.cnt;
+        const int base = (int)link.x, nc = (int)link.y;
         if (st) st->c[RT_STAT_ANY_VOL] += nc;
         for (int c = nc - 1; c >= 0; c--) {
-            if (slab_test(S.nodes[base + c], K, tn)) {
+            if (slab_test(load_node(S.nodes, (uint32_t)(base + c)), K, tn)) {
                 if (sp == STK::CAP) return -1;
                 stk.set_rec(sp++, (uint32_t)(base + c));
             }

@@ -58,19 +58,20 @@ def test_gpu_cfg2_full_frame_rows_match_oracle(manifest, cameras):
 
 def test_gpu_row_shards_bit_identical(manifest, cameras):
     """rt_render_device row shards == rows of the full frame, bit for bit
-    (the multi-GPU partition)."""
-    import torch
+    (the multi-GPU partition). Device memory comes straight
+    from the HIP runtime (no torch in this process)."""
+    from hip_mem import DeviceBuffer
     e = rt_cases.golden_case("cornell32_128", manifest)
     for stride in (2, 3, 8):
         for off in range(stride):
             rk, _ = rt_cases.make_kernel(e, cameras, hostsim=False)
             rows = len(range(off, e["H"], stride))
-            shard = torch.zeros((rows, e["W"], 4), dtype=torch.float32, device="cuda")
-            shard[..., 3] = 1.0
-            torch.cuda.synchronize()
-            rk.render_device(shard.data_ptr(), off, stride, torch.cuda.current_stream().cuda_stream)
-            torch.cuda.synchronize()
-            got = shard.cpu().numpy()
+            init = np.zeros((rows, e["W"], 4), np.float32)
+            init[..., 3] = 1.0
+            buf = DeviceBuffer(init.nbytes)
+            buf.upload(init)
+            rk.render_device(buf.ptr, off, stride, None)
+            got = buf.download(init.shape, np.float32)
             np.testing.assert_array_equal(got.view(np.uint32), e["expected"][off::stride].view(np.uint32))
 
 
