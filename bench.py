@@ -43,6 +43,8 @@ CONFIGS = {
     "cfg3": ("dragon", "L", "dragon", 1920, 1080, 256, 8,
              "PBRT Dragon stand-in 1920x1080x256spp x8 bounces, SKY-L env IS+MIS"),
     "cfg4": ("dragon", "L", "dragon", 3840, 2160, 256, 8, "PBRT Dragon stand-in 3840x2160x256spp x8 bounces"),
+    # profiling-sized cfg2 (same scene / camera / ray mix, 1/16 of the pixels, 1/4 of the samples); not a bench line
+    "cfg2s": ("dragon", "L", "dragon", 480, 270, 16, 8, "profiling-sized cfg2: dragon 480x270x16spp x8"),
 }
 HBM_PEAK_GBS = 8000.0  # /opt/skills/guides/MI355X_MICROARCH.md (spec)
 # SURVEY.md §8(d) byte model: per child-volume test 56 B (7+7 f32 planes),

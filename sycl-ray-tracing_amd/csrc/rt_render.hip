@@ -17,6 +17,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 
 #include "rt_context.h"
@@ -510,6 +511,9 @@ static int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounce
     const int trace_blocks = std::min((3 * n + threads - 1) / threads, dev_cus * 8);
     const int any_blocks = std::min((2 * n + threads - 1) / threads, dev_cus * 8);
     const int ovf_blocks = dev_cus;
+    if (getenv("RT_VERBOSE"))
+        fprintf(stderr, "[rt] run_wave n=%d cus=%d step_blocks=%d trace_blocks=%d any_blocks=%d\n", n, dev_cus,
+                step_blocks, trace_blocks, any_blocks);
     int32_t* ovf_c = W.ovf_closest;
     int32_t* ovf_a = W.ovf_any;
     // each sample takes at most bounces + 1 iterations; +2 for init / final resolve
@@ -649,8 +653,14 @@ int rt_backend_intersect(rt_context* c, const float* rays, int n, void* out)
     int32_t* dout = (int32_t*)((char*)b->xy.p + br);
     HIPCHK(c, hipMemcpy(dr, rays, br, hipMemcpyHostToDevice));
     const int threads = 256, blocks = (n + threads - 1) / threads;
+    HIPCHK(c, hipEventRecord(b->ev0, 0));
     hipLaunchKernelGGL(k_intersect, dim3(blocks), dim3(threads), 0, 0, b->view, dr, dout, n);
     HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipEventRecord(b->ev1, 0));
+    HIPCHK(c, hipEventSynchronize(b->ev1));
+    float ms = 0;
+    HIPCHK(c, hipEventElapsedTime(&ms, b->ev0, b->ev1));
+    c->last_kernel_ms = ms;
     HIPCHK(c, hipMemcpy(out, dout, bo, hipMemcpyDeviceToHost));
     return RT_OK;
 }
