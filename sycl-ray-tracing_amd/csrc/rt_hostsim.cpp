@@ -14,10 +14,14 @@
 #include "rt_context.h"
 #include "rt_wave.h"
 
-// Short-stack capacity of the host build: smaller than the device's so that
-// the CPU tests take the overflow fallback often (dragon rays need up to 19).
+// Stack window and step budget of the host build: smaller than the
+// device's so that the CPU tests exercise spilling (dragon rays need up to
+// 19 entries) and parking / resuming across iterations all the time.
 #ifndef RT_HOSTSIM_SHORT_CAP
 #define RT_HOSTSIM_SHORT_CAP 8
+#endif
+#ifndef RT_HOSTSIM_BUDGET
+#define RT_HOSTSIM_BUDGET 24
 #endif
 
 int rt_backend_create(rt_context*) { return RT_OK; }
@@ -45,6 +49,8 @@ static int run_wave_host(rt_context* c, int w, int h, int spp, int bounces, cons
 {
     if (n <= 0) return RT_OK;
     rtk::WaveView W{};
+    W.park_cap = 1 << 14;
+    W.spill_lanes = 0;  // the host threads keep their own spill areas
     std::vector<char> arena(rtk::wave_carve(nullptr, (size_t)n, W));
     rtk::wave_carve(arena.data(), (size_t)n, W);
     W.S = rt_host_view(c);
@@ -58,9 +64,12 @@ static int run_wave_host(rt_context* c, int w, int h, int spp, int bounces, cons
     W.bl_rays = rt_scene_has_emissive_prim(c) ? 1 : 0;
     W.any_rays = W.S.n_spheres == 0 ? 1 : 0;
     W.fb = fb;
+    W.budget = RT_HOSTSIM_BUDGET;
     int32_t counters[rtk::RK_COUNT] = {0};
     int32_t act[2] = {0, 0};
+    int32_t parkc[2] = {0, 0}, parka[2] = {0, 0};
     W.counters = counters;
+    std::memset(W.r_park, 0, (size_t)n * 4);
     int32_t* lists[2] = {(int32_t*)W.act_in, W.act_out};
     std::vector<rtk::Stats> st(omp_get_max_threads());
     for (auto& s : st) std::memset(&s, 0, sizeof s);
@@ -72,69 +81,88 @@ static int run_wave_host(rt_context* c, int w, int h, int spp, int bounces, cons
         rtk::path_init(W, p, e);
         host_append(W, &act[0], p, e);
     }
-    const long max_iters = (long)spp * ((long)bounces + 1) + 2;
-    for (long it = 0; it < max_iters; it++) {
-        const int cur = (int)(it & 1);
-        const int nc = counters[rtk::RK_CONT] + counters[rtk::RK_LSH] + counters[rtk::RK_BL];
-        const int na = counters[rtk::RK_ESH] + counters[rtk::RK_BENV];
+    using FAST = rtk::ArrayStack<RT_HOSTSIM_SHORT_CAP>;
+    const int last_kind = W.any_rays ? rtk::RK_BL : rtk::RK_BENV;
+    for (long it = 0;; it++) {
+        const int par = (int)(it & 1);
+        W.park_par = par;
+        const int nrc = std::min(parkc[par], W.park_cap), nra = std::min(parka[par], W.park_cap);
+        int nc = nrc, na = nra;
+        for (int k = rtk::RK_CONT; k <= last_kind; k++) nc += counters[k];
+        if (W.any_rays) na += counters[rtk::RK_ESH] + counters[rtk::RK_BENV];
 #pragma omp parallel
         {
-            std::vector<rtk::StackEnt> stack(RT_STACK_CAP);
-            std::vector<uint32_t> astack(RT_STACK_CAP);
-            rtk::ArrayStack<RT_HOSTSIM_SHORT_CAP> sstack;
+            std::vector<uint32_t> spr(RT_STACK_CAP);
+            std::vector<float> spk(RT_STACK_CAP);
+            rtk::SpillStack<FAST> stk{FAST{}, spr.data(), spk.data()};
             rtk::Stats* ps = c->stats_enabled ? &st[omp_get_thread_num()] : nullptr;
-#pragma omp for schedule(dynamic, 64)
+#pragma omp for schedule(dynamic, 16)
             for (int idx = 0; idx < nc; idx++) {
-                int kind = rtk::RK_CONT, i = idx;
-                if (i >= counters[rtk::RK_CONT]) {
-                    i -= counters[rtk::RK_CONT];
-                    kind = rtk::RK_LSH;
-                    if (i >= counters[rtk::RK_LSH]) {
-                        i -= counters[rtk::RK_LSH];
-                        kind = rtk::RK_BL;
+                rtk::TravC T;
+                uint32_t target;
+                bool resumed = idx < nrc, has;
+                if (resumed) {
+                    target = rtk::travc_resume(&W.park_c[par][idx], T, stk);
+                    has = true;
+                } else {
+                    const rtk::RayRec r = rtk::queue_item(W, counters, rtk::RK_CONT, last_kind, idx - nrc, target);
+                    has = rtk::travc_begin(W.S, T, rtk::v3of(r.o), rtk::v3of(r.d), ps);
+                    if (!has) rtk::finish_closest(W, target, T.o, T.d, T.best_t, T.best_k);
+                }
+                while (has) {
+                    if (!rtk::travc_step(W.S, T, stk, ps)) {
+                        rtk::finish_closest(W, target, T.o, T.d, T.best_t, T.best_k);
+                        if (resumed) __atomic_fetch_sub(&W.r_park[target >> 3], 1, __ATOMIC_RELAXED);
+                        break;
+                    }
+                    if (T.steps >= W.budget && rtk::travc_parkable(T)) {
+                        const int slot = __atomic_fetch_add(&parkc[par ^ 1], 1, __ATOMIC_RELAXED);
+                        if (slot < W.park_cap) {
+                            rtk::travc_park(T, stk, target, &W.park_c[par ^ 1][slot]);
+                            if (!resumed) __atomic_fetch_add(&W.r_park[target >> 3], 1, __ATOMIC_RELAXED);
+                            break;
+                        }
+                        T.steps = 0;
                     }
                 }
-                const rtk::RayRec r = W.q[kind][i];
-                const int slot = (int)rt_asuint(r.o.w);
-                float t;
-                int k;
-                // a small short stack so the tests exercise the overflow fallback
-                if (!rtk::query_closest_short(W.S, rtk::v3of(r.o), rtk::v3of(r.d), sstack, t, k, ps))
-                    rtk::query_closest(W.S, rtk::v3of(r.o), rtk::v3of(r.d), stack.data(), t, k, ps);
-                if (kind == rtk::RK_CONT) {
-                    W.r_cont_t[slot] = t;
-                    W.r_cont_k[slot] = k;
-                } else if (kind == rtk::RK_LSH) {
-                    W.r_lsh_t[slot] = t;
-                } else {
-                    W.r_bl_t[slot] = t;
-                    W.r_bl_k[slot] = k;
-                }
             }
-#pragma omp for schedule(dynamic, 64)
+#pragma omp for schedule(dynamic, 16)
             for (int idx = 0; idx < na; idx++) {
-                const int n0 = counters[rtk::RK_ESH];
-                const int kind = idx < n0 ? rtk::RK_ESH : rtk::RK_BENV;
-                const rtk::RayRec r = W.q[kind][idx < n0 ? idx : idx - n0];
-                const int slot = (int)rt_asuint(r.o.w);
-                bool hit;
-                if (W.any_rays) {
-                    const int a = rtk::trace_any_short(W.S, rtk::v3of(r.o), rtk::v3of(r.d), sstack, ps);
-                    hit = a >= 0 ? a == 1 : rtk::trace_any(W.S, rtk::v3of(r.o), rtk::v3of(r.d), astack.data(), ps);
+                rtk::TravA T;
+                uint32_t target;
+                bool resumed = idx < nra, has;
+                if (resumed) {
+                    target = rtk::trava_resume(&W.park_a[par][idx], T, stk);
+                    has = true;
                 } else {
-                    float t;
-                    int k;
-                    rtk::query_closest(W.S, rtk::v3of(r.o), rtk::v3of(r.d), stack.data(), t, k, ps);
-                    hit = t > 0.0f;
+                    const rtk::RayRec r = rtk::queue_item(W, counters, rtk::RK_ESH, rtk::RK_BENV, idx - nra, target);
+                    has = rtk::trava_begin(W.S, T, rtk::v3of(r.o), rtk::v3of(r.d), ps);
+                    if (!has) rtk::finish_any(W, target, false);
                 }
-                (kind == rtk::RK_ESH ? W.r_esh : W.r_benv)[slot] = hit ? 1 : 0;
+                while (has) {
+                    if (!rtk::trava_step(W.S, T, stk, ps)) {
+                        rtk::finish_any(W, target, T.hit);
+                        if (resumed) __atomic_fetch_sub(&W.r_park[target >> 3], 1, __ATOMIC_RELAXED);
+                        break;
+                    }
+                    if (T.steps >= W.budget && rtk::trava_parkable(T)) {
+                        const int slot = __atomic_fetch_add(&parka[par ^ 1], 1, __ATOMIC_RELAXED);
+                        if (slot < W.park_cap) {
+                            rtk::trava_park(T, stk, target, &W.park_a[par ^ 1][slot]);
+                            if (!resumed) __atomic_fetch_add(&W.r_park[target >> 3], 1, __ATOMIC_RELAXED);
+                            break;
+                        }
+                        T.steps = 0;
+                    }
+                }
             }
         }
         for (int k = 0; k < rtk::RK_COUNT; k++) counters[k] = 0;
-        act[cur ^ 1] = 0;
-        W.act_in = lists[cur];
-        W.act_out = lists[cur ^ 1];
-        const int n_in = act[cur];
+        parkc[par] = parka[par] = 0;
+        act[par ^ 1] = 0;
+        W.act_in = lists[par];
+        W.act_out = lists[par ^ 1];
+        const int n_in = act[par];
         if (n_in == 0) break;
 #pragma omp parallel
         {
@@ -144,7 +172,7 @@ static int run_wave_host(rt_context* c, int w, int h, int spp, int bounces, cons
                 const int p = W.act_in[idx];
                 rtk::Emit e;
                 rtk::path_step(W, p, e, ps);
-                host_append(W, &act[cur ^ 1], p, e);
+                host_append(W, &act[par ^ 1], p, e);
             }
         }
     }

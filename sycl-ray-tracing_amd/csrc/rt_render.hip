@@ -45,10 +45,12 @@ enum {
     C_TK_CLOSEST = rtk::RK_COUNT,
     C_TK_ANY,
     C_TK_STEP,
-    C_OVF_CLOSEST,            // rays whose short stack overflowed (re-traced by the fallback kernels)
-    C_OVF_ANY,
     C_ACT0,                   // live-slot counts, double-buffered
     C_ACT1,
+    C_PARKC0,                 // parked queries, double-buffered by iteration parity
+    C_PARKC1,
+    C_PARKA0,
+    C_PARKA1,
     C_COUNT
 };
 
@@ -64,6 +66,7 @@ struct Backend {
     RtSceneView view{};
     int bl_rays = 1, any_rays = 1;
     int last_iters = 0;
+    int budget = 1024;  // steps per query per launch before it parks (RT_STEP_BUDGET)
     // optional per-kernel timing: events around each launch of each class
     bool timing = false;
     hipEvent_t tev[4][RT_MAX_TIMED_ITERS] = {};
@@ -128,7 +131,7 @@ struct LdsStack {
     __device__ __forceinline__ void set_rec(int i, uint32_t rv) { r[i * 256] = rv; }
 };
 #define RT_LDS_CAP_CLOSEST 16
-#define RT_LDS_CAP_ANY 24
+#define RT_LDS_CAP_ANY 16
 
 // One ticket of 64 work items per wave.
 __device__ __forceinline__ int wave_ticket(int32_t* ticket)
@@ -197,153 +200,154 @@ __global__ __launch_bounds__(256) void k_step(rtk::WaveView W, const int32_t* ac
     flush_stats<STATS>(st, stats);
 }
 
-// Decodes a closest-hit work index into (kind, queue position).
-__device__ __forceinline__ int closest_kind(const rtk::WaveView& W, int& i)
-{
-    const int n0 = W.counters[C_Q0 + rtk::RK_CONT], n1 = W.counters[C_Q0 + rtk::RK_LSH];
-    if (i < n0) return rtk::RK_CONT;
-    i -= n0;
-    if (i < n1) return rtk::RK_LSH;
-    i -= n1;
-    return rtk::RK_BL;
-}
+// ------------------------------------------------------------- trace kernels
+// Persistent waves; each lane runs one query at a time, one unit of work per
+// loop trip (rt_traverse.h). Idle lanes refill from the work list (parked
+// queries of the last launch first, then the queues) once REFILL lanes are
+// idle; a query that has taken W.budget steps parks at its next node
+// boundary. Work list order: parked, then the ray kinds in queue order.
+#define RT_REFILL 16
 
-__device__ __forceinline__ void store_closest(const rtk::WaveView& W, int kind, int slot, float t, int k)
-{
-    if (kind == rtk::RK_CONT) {
-        W.r_cont_t[slot] = t;
-        W.r_cont_k[slot] = k;
-    } else if (kind == rtk::RK_LSH) {
-        W.r_lsh_t[slot] = t;
-    } else {
-        W.r_bl_t[slot] = t;
-        W.r_bl_k[slot] = k;
-    }
-}
-
-// Closest-hit queries with the LDS short stack; overflowing rays go to the
-// fallback queue (k_trace_closest_ovf, unbounded scratch stack).
 template <bool STATS>
-__global__ __launch_bounds__(256, 5) void k_trace_closest(rtk::WaveView W, int32_t* ovf, unsigned long long* stats)
+__global__ __launch_bounds__(256, 4) void k_trace_closest(rtk::WaveView W, unsigned long long* stats)
 {
     __shared__ uint32_t s_r[RT_LDS_CAP_CLOSEST * 256];
     __shared__ float s_k[RT_LDS_CAP_CLOSEST * 256];
-    LdsStack<RT_LDS_CAP_CLOSEST> stk{s_r + threadIdx.x, s_k + threadIdx.x};
-    const int total = W.counters[C_Q0 + rtk::RK_CONT] + W.counters[C_Q0 + rtk::RK_LSH] +
-                      W.counters[C_Q0 + rtk::RK_BL];
+    using FAST = LdsStack<RT_LDS_CAP_CLOSEST>;
+    const int gl = blockIdx.x * blockDim.x + threadIdx.x;
+    rtk::SpillStack<FAST> stk{FAST{s_r + threadIdx.x, s_k + threadIdx.x}, W.spill_r + (size_t)gl * RT_STACK_CAP,
+                              W.spill_k + (size_t)gl * RT_STACK_CAP};
+    const int par = W.park_par;
+    const int n_res = min(W.counters[C_PARKC0 + par], W.park_cap);
+    const int last_kind = W.any_rays ? rtk::RK_BL : rtk::RK_BENV;
+    int total = n_res;
+    for (int k = rtk::RK_CONT; k <= last_kind; k++) total += W.counters[C_Q0 + k];
     rtk::Stats st;
     if (STATS)
         for (int i = 0; i < RT_STAT_COUNT; i++) st.c[i] = 0;
+    rtk::TravC T;
+    bool has = false, resumed = false, drained = false;
+    uint32_t target = 0;
     for (;;) {
-        const int base = wave_ticket(W.counters + C_TK_CLOSEST);
-        if (base >= total) break;
-        const int idx = base + lane_id();
-        bool over = false;
-        if (idx < total) {
-            int i = idx;
-            const int kind = closest_kind(W, i);
-            const rtk::RayRec r = W.q[kind][i];
-            float t;
-            int k;
-            if (rtk::query_closest_short(W.S, rtk::v3of(r.o), rtk::v3of(r.d), stk, t, k, STATS ? &st : nullptr))
-                store_closest(W, kind, (int)rt_asuint(r.o.w), t, k);
-            else
-                over = true;
-        }
-        const int o = wave_append(W.counters + C_OVF_CLOSEST, over);
-        if (over) ovf[o] = idx;
-    }
-    flush_stats<STATS>(st, stats);
-}
-
-template <bool STATS>
-__global__ __launch_bounds__(256) void k_trace_closest_ovf(rtk::WaveView W, const int32_t* ovf,
-                                                           unsigned long long* stats)
-{
-    const int n = W.counters[C_OVF_CLOSEST];
-    rtk::StackEnt stack[RT_STACK_CAP];
-    rtk::Stats st;
-    if (STATS)
-        for (int i = 0; i < RT_STAT_COUNT; i++) st.c[i] = 0;
-    for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += gridDim.x * blockDim.x) {
-        int i = ovf[j];
-        const int kind = closest_kind(W, i);
-        const rtk::RayRec r = W.q[kind][i];
-        float t;
-        int k;
-        rtk::query_closest(W.S, rtk::v3of(r.o), rtk::v3of(r.d), stack, t, k, STATS ? &st : nullptr);
-        store_closest(W, kind, (int)rt_asuint(r.o.w), t, k);
-    }
-    flush_stats<STATS>(st, stats);
-}
-
-// Occlusion queries. ANY: the any-hit walk with an LDS short stack
-// (overflow -> k_trace_any_ovf); !ANY (analytic spheres present): the exact
-// closest-hit logic with an unbounded stack.
-template <bool STATS, bool ANY>
-__global__ __launch_bounds__(256) void k_trace_any(rtk::WaveView W, int32_t* ovf, unsigned long long* stats)
-{
-    __shared__ uint32_t s_r[ANY ? RT_LDS_CAP_ANY * 256 : 1];
-    LdsStack<RT_LDS_CAP_ANY> stk{s_r + (ANY ? threadIdx.x : 0), nullptr};
-    const int n0 = W.counters[C_Q0 + rtk::RK_ESH], n1 = W.counters[C_Q0 + rtk::RK_BENV];
-    const int total = n0 + n1;
-    rtk::StackEnt cstack[ANY ? 1 : RT_STACK_CAP];
-    rtk::Stats st;
-    if (STATS)
-        for (int i = 0; i < RT_STAT_COUNT; i++) st.c[i] = 0;
-    for (;;) {
-        const int base = wave_ticket(W.counters + C_TK_ANY);
-        if (base >= total) break;
-        const int idx = base + lane_id();
-        bool over = false;
-        if (idx < total) {
-            const int kind = idx < n0 ? rtk::RK_ESH : rtk::RK_BENV;
-            const rtk::RayRec r = W.q[kind][idx < n0 ? idx : idx - n0];
-            const int slot = (int)rt_asuint(r.o.w);
-            int hit;
-            if (ANY) {
-                hit = rtk::trace_any_short(W.S, rtk::v3of(r.o), rtk::v3of(r.d), stk, STATS ? &st : nullptr);
-            } else {
-                float t;
-                int k;
-                rtk::query_closest(W.S, rtk::v3of(r.o), rtk::v3of(r.d), cstack, t, k, STATS ? &st : nullptr);
-                hit = t > 0.0f ? 1 : 0;
+        const bool need = !has;
+        const unsigned long long bneed = __ballot(need);
+        const int nneed = __popcll(bneed);
+        if (!drained && (nneed >= RT_REFILL || nneed == 64)) {
+            int base = 0;
+            if (lane_id() == 0) base = atomicAdd(W.counters + C_TK_CLOSEST, nneed);
+            base = __shfl(base, 0);
+            if (base + nneed >= total) drained = true;
+            if (need) {
+                const int idx = base + __popcll(bneed & ((1ull << lane_id()) - 1ull));
+                if (idx < n_res) {
+                    target = rtk::travc_resume(&W.park_c[par][idx], T, stk);
+                    has = resumed = true;
+                } else if (idx < total) {
+                    const rtk::RayRec r = rtk::queue_item(W, W.counters + C_Q0, rtk::RK_CONT, last_kind, idx - n_res,
+                                                          target);
+                    resumed = false;
+                    has = rtk::travc_begin(W.S, T, rtk::v3of(r.o), rtk::v3of(r.d), STATS ? &st : nullptr);
+                    if (!has) rtk::finish_closest(W, target, T.o, T.d, T.best_t, T.best_k);
+                }
             }
-            if (hit >= 0)
-                (kind == rtk::RK_ESH ? W.r_esh : W.r_benv)[slot] = (uint8_t)hit;
-            else
-                over = true;
         }
-        const int o = wave_append(W.counters + C_OVF_ANY, over);
-        if (over) ovf[o] = idx;
+        if (!__any(has)) {
+            if (drained) break;
+            continue;
+        }
+        if (has) {
+            if (!rtk::travc_step(W.S, T, stk, STATS ? &st : nullptr)) {
+                rtk::finish_closest(W, target, T.o, T.d, T.best_t, T.best_k);
+                if (resumed) atomicSub(&W.r_park[target >> 3], 1);
+                has = false;
+            } else if (T.steps >= W.budget && rtk::travc_parkable(T)) {
+                const int ps = atomicAdd(W.counters + C_PARKC0 + (par ^ 1), 1);
+                if (ps < W.park_cap) {
+                    rtk::travc_park(T, stk, target, &W.park_c[par ^ 1][ps]);
+                    if (!resumed) atomicAdd(&W.r_park[target >> 3], 1);
+                    has = false;
+                } else {
+                    T.steps = 0;  // park pool full: keep going
+                }
+            }
+        }
     }
     flush_stats<STATS>(st, stats);
 }
 
 template <bool STATS>
-__global__ __launch_bounds__(256) void k_trace_any_ovf(rtk::WaveView W, const int32_t* ovf, unsigned long long* stats)
+__global__ __launch_bounds__(256, 4) void k_trace_any(rtk::WaveView W, unsigned long long* stats)
 {
-    const int n = W.counters[C_OVF_ANY];
-    const int n0 = W.counters[C_Q0 + rtk::RK_ESH];
-    uint32_t stack[RT_STACK_CAP];
+    __shared__ uint32_t s_r[RT_LDS_CAP_ANY * 256];
+    using FAST = LdsStack<RT_LDS_CAP_ANY>;
+    const int gl = blockIdx.x * blockDim.x + threadIdx.x;
+    rtk::SpillStack<FAST> stk{FAST{s_r + threadIdx.x, nullptr}, W.spill_r + (size_t)gl * RT_STACK_CAP, nullptr};
+    const int par = W.park_par;
+    const int n_res = min(W.counters[C_PARKA0 + par], W.park_cap);
+    const int total = n_res + W.counters[C_Q0 + rtk::RK_ESH] + W.counters[C_Q0 + rtk::RK_BENV];
     rtk::Stats st;
     if (STATS)
         for (int i = 0; i < RT_STAT_COUNT; i++) st.c[i] = 0;
-    for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += gridDim.x * blockDim.x) {
-        const int idx = ovf[j];
-        const int kind = idx < n0 ? rtk::RK_ESH : rtk::RK_BENV;
-        const rtk::RayRec r = W.q[kind][idx < n0 ? idx : idx - n0];
-        const bool hit = rtk::trace_any(W.S, rtk::v3of(r.o), rtk::v3of(r.d), stack, STATS ? &st : nullptr);
-        (kind == rtk::RK_ESH ? W.r_esh : W.r_benv)[(int)rt_asuint(r.o.w)] = hit ? 1 : 0;
+    rtk::TravA T;
+    bool has = false, resumed = false, drained = false;
+    uint32_t target = 0;
+    for (;;) {
+        const bool need = !has;
+        const unsigned long long bneed = __ballot(need);
+        const int nneed = __popcll(bneed);
+        if (!drained && (nneed >= RT_REFILL || nneed == 64)) {
+            int base = 0;
+            if (lane_id() == 0) base = atomicAdd(W.counters + C_TK_ANY, nneed);
+            base = __shfl(base, 0);
+            if (base + nneed >= total) drained = true;
+            if (need) {
+                const int idx = base + __popcll(bneed & ((1ull << lane_id()) - 1ull));
+                if (idx < n_res) {
+                    target = rtk::trava_resume(&W.park_a[par][idx], T, stk);
+                    has = resumed = true;
+                } else if (idx < total) {
+                    const rtk::RayRec r = rtk::queue_item(W, W.counters + C_Q0, rtk::RK_ESH, rtk::RK_BENV,
+                                                          idx - n_res, target);
+                    resumed = false;
+                    has = rtk::trava_begin(W.S, T, rtk::v3of(r.o), rtk::v3of(r.d), STATS ? &st : nullptr);
+                    if (!has) rtk::finish_any(W, target, false);
+                }
+            }
+        }
+        if (!__any(has)) {
+            if (drained) break;
+            continue;
+        }
+        if (has) {
+            if (!rtk::trava_step(W.S, T, stk, STATS ? &st : nullptr)) {
+                rtk::finish_any(W, target, T.hit);
+                if (resumed) atomicSub(&W.r_park[target >> 3], 1);
+                has = false;
+            } else if (T.steps >= W.budget && rtk::trava_parkable(T)) {
+                const int ps = atomicAdd(W.counters + C_PARKA0 + (par ^ 1), 1);
+                if (ps < W.park_cap) {
+                    rtk::trava_park(T, stk, target, &W.park_a[par ^ 1][ps]);
+                    if (!resumed) atomicAdd(&W.r_park[target >> 3], 1);
+                    has = false;
+                } else {
+                    T.steps = 0;
+                }
+            }
+        }
     }
     flush_stats<STATS>(st, stats);
 }
 
-__global__ void k_reset(int32_t* counters, int act_slot)
+// Between the trace launches and the step of an iteration: queue sizes and
+// tickets, the live count the step will write, and the park counts the
+// trace launches just consumed.
+__global__ void k_reset(int32_t* counters, int act_slot, int park_par)
 {
     const int i = threadIdx.x;
     if (i < C_ACT0) counters[i] = 0;
     if (i == 0) counters[act_slot] = 0;
+    if (i == 1) counters[C_PARKC0 + park_par] = 0;
+    if (i == 2) counters[C_PARKA0 + park_par] = 0;
 }
 
 __global__ __launch_bounds__(256) void k_intersect(RtSceneView S, const float* __restrict__ rays, int32_t* __restrict__ out,
@@ -414,6 +418,7 @@ int rt_backend_create(rt_context* c)
     HIPCHK(c, hipEventCreate(&b->ev0));
     HIPCHK(c, hipEventCreate(&b->ev1));
     HIPCHK(c, hipHostMalloc((void**)&b->h_act, 16, hipHostMallocDefault));
+    if (const char* e = getenv("RT_STEP_BUDGET")) b->budget = std::max(1, atoi(e));
     return RT_OK;
 }
 
@@ -476,7 +481,14 @@ static int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounce
                     float4_* fb, hipStream_t s)
 {
     if (n <= 0) return RT_OK;
+    int dev_cus = 256;
+    (void)hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, c->device);
+    const int threads = 256;
+    const int step_blocks = std::min((n + threads - 1) / threads, dev_cus * 8);
+    const int trace_blocks = dev_cus * 4;  // persistent: 4 blocks of 256 per CU (LDS stacks, 4 waves/SIMD)
     rtk::WaveView W{};
+    W.park_cap = 1 << 16;
+    W.spill_lanes = trace_blocks * threads;
     const size_t need = rtk::wave_carve(nullptr, (size_t)n, W);
     if (int r = ensure(c, b->wave, need)) return r;
     rtk::wave_carve((char*)b->wave.p, (size_t)n, W);
@@ -491,68 +503,50 @@ static int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounce
     W.bl_rays = b->bl_rays;
     W.any_rays = b->any_rays;
     W.fb = fb;
+    W.budget = b->budget;
     W.counters = (int32_t*)b->counters.p;
     int32_t* lists[2] = {(int32_t*)W.act_in, W.act_out};
     int32_t* cnt = (int32_t*)b->counters.p;
     unsigned long long* stats = (unsigned long long*)b->stats.p;
     const bool S = c->stats_enabled;
     if (S) HIPCHK(c, hipMemsetAsync(b->stats.p, 0, b->stats.bytes, s));
+    if (getenv("RT_VERBOSE"))
+        fprintf(stderr, "[rt] run_wave n=%d cus=%d step_blocks=%d trace_blocks=%d budget=%d wave_bytes=%zu\n", n,
+                dev_cus, step_blocks, trace_blocks, W.budget, need);
 
     HIPCHK(c, hipMemsetAsync(cnt, 0, C_COUNT * sizeof(int32_t), s));
+    HIPCHK(c, hipMemsetAsync(W.r_park, 0, (size_t)n * 4, s));
     W.act_in = lists[1];
     W.act_out = lists[0];
-    const int threads = 256;
     hipLaunchKernelGGL(k_init, dim3((n + threads - 1) / threads), dim3(threads), 0, s, W, cnt + C_ACT0);
     HIPCHK(c, hipGetLastError());
 
-    int dev_cus = 256;
-    (void)hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, c->device);
-    const int step_blocks = std::min((n + threads - 1) / threads, dev_cus * 8);
-    const int trace_blocks = std::min((3 * n + threads - 1) / threads, dev_cus * 8);
-    const int any_blocks = std::min((2 * n + threads - 1) / threads, dev_cus * 8);
-    const int ovf_blocks = dev_cus;
-    if (getenv("RT_VERBOSE"))
-        fprintf(stderr, "[rt] run_wave n=%d cus=%d step_blocks=%d trace_blocks=%d any_blocks=%d\n", n, dev_cus,
-                step_blocks, trace_blocks, any_blocks);
-    int32_t* ovf_c = W.ovf_closest;
-    int32_t* ovf_a = W.ovf_any;
-    // each sample takes at most bounces + 1 iterations; +2 for init / final resolve
-    long max_iters = (long)spp * ((long)bounces + 1) + 2;
-    if (b->timing) {
-        if (max_iters > RT_MAX_TIMED_ITERS) return rt_fail(c, RT_ERR_ARG, "kernel timing: too many iterations");
-        for (int k = 0; k < 4; k++)
-            for (long i = 0; i < max_iters; i++)
-                if (!b->tev[k][i]) HIPCHK(c, hipEventCreate(&b->tev[k][i]));
-    }
+    // A sample takes at most bounces + 1 iterations without parking; parked
+    // queries stretch that. The bound only guards against a runaway loop.
+    const long max_iters = 64l * spp * ((long)bounces + 1) + 4096;
     int it = 0;
-    for (; it < max_iters; it++) {
+    bool done = false;
+    for (; it < max_iters && !done; it++) {
         const int cur = it & 1;
-        const bool T = b->timing;
+        const bool T = b->timing && it < RT_MAX_TIMED_ITERS;
+        if (T)
+            for (int k = 0; k < 4; k++)
+                if (!b->tev[k][it]) HIPCHK(c, hipEventCreate(&b->tev[k][it]));
+        W.park_par = cur;
         if (T) HIPCHK(c, hipEventRecord(b->tev[0][it], s));
-        if (S) {
-            hipLaunchKernelGGL(k_trace_closest<true>, dim3(trace_blocks), dim3(threads), 0, s, W, ovf_c, stats);
-            hipLaunchKernelGGL(k_trace_closest_ovf<true>, dim3(ovf_blocks), dim3(threads), 0, s, W, ovf_c, stats);
-        } else {
-            hipLaunchKernelGGL(k_trace_closest<false>, dim3(trace_blocks), dim3(threads), 0, s, W, ovf_c, stats);
-            hipLaunchKernelGGL(k_trace_closest_ovf<false>, dim3(ovf_blocks), dim3(threads), 0, s, W, ovf_c, stats);
-        }
-        if (T) HIPCHK(c, hipEventRecord(b->tev[1][it], s));
-        if (S && W.any_rays)
-            hipLaunchKernelGGL((k_trace_any<true, true>), dim3(any_blocks), dim3(threads), 0, s, W, ovf_a, stats);
-        else if (S)
-            hipLaunchKernelGGL((k_trace_any<true, false>), dim3(any_blocks), dim3(threads), 0, s, W, ovf_a, stats);
-        else if (W.any_rays)
-            hipLaunchKernelGGL((k_trace_any<false, true>), dim3(any_blocks), dim3(threads), 0, s, W, ovf_a, stats);
+        if (S)
+            hipLaunchKernelGGL(k_trace_closest<true>, dim3(trace_blocks), dim3(threads), 0, s, W, stats);
         else
-            hipLaunchKernelGGL((k_trace_any<false, false>), dim3(any_blocks), dim3(threads), 0, s, W, ovf_a, stats);
+            hipLaunchKernelGGL(k_trace_closest<false>, dim3(trace_blocks), dim3(threads), 0, s, W, stats);
+        if (T) HIPCHK(c, hipEventRecord(b->tev[1][it], s));
         if (W.any_rays) {
             if (S)
-                hipLaunchKernelGGL(k_trace_any_ovf<true>, dim3(ovf_blocks), dim3(threads), 0, s, W, ovf_a, stats);
+                hipLaunchKernelGGL(k_trace_any<true>, dim3(trace_blocks), dim3(threads), 0, s, W, stats);
             else
-                hipLaunchKernelGGL(k_trace_any_ovf<false>, dim3(ovf_blocks), dim3(threads), 0, s, W, ovf_a, stats);
+                hipLaunchKernelGGL(k_trace_any<false>, dim3(trace_blocks), dim3(threads), 0, s, W, stats);
         }
         if (T) HIPCHK(c, hipEventRecord(b->tev[2][it], s));
-        hipLaunchKernelGGL(k_reset, dim3(1), dim3(64), 0, s, cnt, C_ACT0 + (cur ^ 1));
+        hipLaunchKernelGGL(k_reset, dim3(1), dim3(64), 0, s, cnt, C_ACT0 + (cur ^ 1), cur);
         // step: reads the list written last iteration (lists[cur]) -> lists[cur ^ 1]
         W.act_in = lists[cur];
         W.act_out = lists[cur ^ 1];
@@ -567,10 +561,14 @@ static int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounce
         if ((it & 7) == 7) {
             HIPCHK(c, hipMemcpyAsync(b->h_act, cnt + C_ACT0 + (cur ^ 1), 4, hipMemcpyDeviceToHost, s));
             HIPCHK(c, hipStreamSynchronize(s));
-            if (*b->h_act == 0) break;
+            done = *b->h_act == 0;
         }
     }
-    b->last_iters = it + 1;
+    if (!done) {
+        HIPCHK(c, hipStreamSynchronize(s));
+        return rt_fail(c, RT_ERR_STATE, "render: wavefront loop did not drain");
+    }
+    b->last_iters = it;
     if (b->timing) {  // per-kernel-class time of this render (HIP events on its stream)
         HIPCHK(c, hipStreamSynchronize(s));
         for (int i = 0; i < b->last_iters && i < RT_MAX_TIMED_ITERS; i++)

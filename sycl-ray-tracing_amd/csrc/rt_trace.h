@@ -105,8 +105,8 @@ struct Stats {
 // finite operand (tests: test_gpu_parity.py::test_gpu_slab_division_exact).
 // On gfx950 that is 3 instructions instead of the ~10 of an IEEE f32 divide.
 struct RayK {
-    float den[7], num[7];
-    double rinv[7];
+    float num[7];
+    double rinv[7];  // 1/den: +-inf exactly when den == 0, negative exactly when den < 0
 };
 
 RT_HD float slab_div(float a, double rinv) { return (float)((double)a * rinv); }
@@ -118,10 +118,10 @@ RT_HD bool ray_setup(V3 o, V3 d, RayK& k)
     bool bad = false;
 #pragma unroll
     for (int i = 0; i < 7; i++) {
-        k.den[i] = dot(N[i], d);
+        const float den = dot(N[i], d);
         k.num[i] = dot(N[i], o);
-        k.rinv[i] = 1.0 / (double)k.den[i];
-        bad = bad || rt_isnan(k.den[i]) || rt_isnan(k.num[i]);
+        k.rinv[i] = 1.0 / (double)den;
+        bad = bad || rt_isnan(den) || rt_isnan(k.num[i]);
     }
     // A NaN component makes every slab test pass and every triangle test
     // fail (NaN compares false), so such a ray can never hit.
@@ -170,11 +170,11 @@ RT_HD bool slab_test(const NodeR& nd, const RayK& k, float& tnear)
     float tn = -__builtin_inff(), tf = __builtin_inff();
 #pragma unroll
     for (int i = 0; i < 7; i++) {
-        const float d = k.den[i];
-        const bool neg = d < 0.0f;
-        float a = slab_div((neg ? nd.df[i] : nd.dn[i]) - k.num[i], k.rinv[i]);
-        float b = slab_div((neg ? nd.dn[i] : nd.df[i]) - k.num[i], k.rinv[i]);
-        if (d == 0.0f) {
+        const double r = k.rinv[i];
+        const bool neg = r < 0.0;
+        float a = slab_div((neg ? nd.df[i] : nd.dn[i]) - k.num[i], r);
+        float b = slab_div((neg ? nd.dn[i] : nd.df[i]) - k.num[i], r);
+        if (__builtin_isinf(r)) {  // den == 0: the reference skips the plane
             a = -__builtin_inff();
             b = __builtin_inff();
         }

@@ -20,7 +20,7 @@
 // the launch's pixel source): 16-B records so a wave's loads coalesce.
 #pragma once
 
-#include "rt_trace.h"
+#include "rt_traverse.h"
 
 namespace rtk {
 
@@ -97,8 +97,15 @@ struct WaveView {
     // queues
     RayRec* q[RK_COUNT];    // [n_slots] each
     int32_t* counters;      // queue sizes, tickets, live counts (rt_render.hip C_*)
-    int32_t* ovf_closest;   // [3 n_slots] closest-hit work items whose short stack overflowed
-    int32_t* ovf_any;       // [2 n_slots] occlusion work items whose short stack overflowed
+    int32_t* r_park;        // [n_slots] queries of the slot parked (the step skips the slot while > 0)
+    ParkC* park_c[2];       // parked closest-hit queries, double-buffered by iteration parity
+    ParkA* park_a[2];
+    int park_cap;
+    int park_par;           // parity this iteration reads
+    int budget;             // steps a query may take per launch before it parks
+    uint32_t* spill_r;      // per-lane stack spill areas of the trace kernels
+    float* spill_k;
+    int spill_lanes;
     const int32_t* act_in;  // active slots this iteration
     int32_t* act_out;
     int n_act_in;
@@ -106,7 +113,7 @@ struct WaveView {
 
 // Carves the path-slot buffers for n slots out of one allocation at `base`
 // (nullptr: only sizes it). Returns the bytes needed.
-inline size_t wave_carve(char* base, size_t n, WaveView& W)
+inline size_t wave_carve(char* base, size_t n, WaveView& W)  // uses W.park_cap, W.spill_lanes
 {
     size_t o = 0;
     auto take = [&](size_t bytes) -> void* {
@@ -138,8 +145,13 @@ inline size_t wave_carve(char* base, size_t n, WaveView& W)
     for (int k = 0; k < RK_COUNT; k++) W.q[k] = (RayRec*)take(n * sizeof(RayRec));
     W.act_in = (const int32_t*)take(n * 4);
     W.act_out = (int32_t*)take(n * 4);
-    W.ovf_closest = (int32_t*)take(3 * n * 4);
-    W.ovf_any = (int32_t*)take(2 * n * 4);
+    W.r_park = (int32_t*)take(n * 4);
+    for (int k = 0; k < 2; k++) {
+        W.park_c[k] = (ParkC*)take((size_t)W.park_cap * sizeof(ParkC));
+        W.park_a[k] = (ParkA*)take((size_t)W.park_cap * sizeof(ParkA));
+    }
+    W.spill_r = (uint32_t*)take((size_t)W.spill_lanes * RT_STACK_CAP * 4);
+    W.spill_k = (float*)take((size_t)W.spill_lanes * RT_STACK_CAP * 4);
     return o;
 }
 
@@ -498,6 +510,9 @@ RT_HD void resolve(const WaveView& W, int p, PathReg& P, Stats* st)
 // start the next sample. Fills `e` with the rays for the next trace.
 RT_HD void path_step(const WaveView& W, int p, Emit& e, Stats* st)
 {
+    e.mask = 0;
+    e.active = true;
+    if (W.r_park[p] != 0) return;  // a query of this path is parked: wait
     PathReg P;
     load_path(W, p, P);
     e.mask = 0;
@@ -549,6 +564,48 @@ RT_HD void query_closest(const RtSceneView& S, V3 o, V3 d, StackEnt* stack, floa
 {
     trace_closest(S, o, d, stack, t, k, st);
     spheres_closest(S, o, d, t, k);
+}
+
+// Writes a finished closest-hit query (octree best + sphere loop) to its
+// result slot; target = slot * 8 + kind. Occlusion kinds reach here only
+// when analytic spheres are present (then they use the exact closest logic).
+RT_HD void finish_closest(const WaveView& W, uint32_t target, V3 o, V3 d, float t, int k)
+{
+    spheres_closest(W.S, o, d, t, k);
+    const int slot = (int)(target >> 3), kind = (int)(target & 7u);
+    if (kind == RK_CONT) {
+        W.r_cont_t[slot] = t;
+        W.r_cont_k[slot] = k;
+    } else if (kind == RK_LSH) {
+        W.r_lsh_t[slot] = t;
+    } else if (kind == RK_BL) {
+        W.r_bl_t[slot] = t;
+        W.r_bl_k[slot] = k;
+    } else {
+        (kind == RK_ESH ? W.r_esh : W.r_benv)[slot] = t > 0.0f ? 1 : 0;
+    }
+}
+
+RT_HD void finish_any(const WaveView& W, uint32_t target, bool hit)
+{
+    const int slot = (int)(target >> 3), kind = (int)(target & 7u);
+    (kind == RK_ESH ? W.r_esh : W.r_benv)[slot] = hit ? 1 : 0;
+}
+
+// The queue item behind a trace work index: closest-hit kernels see
+// CONT, LSH, BL (then ESH, BENV when they need the closest logic); the
+// occlusion kernel sees ESH, BENV. Returns the ray and its target.
+RT_HD RayRec queue_item(const WaveView& W, const int32_t* counts, int first_kind, int last_kind, int i,
+                        uint32_t& target)
+{
+    int kind = first_kind;
+    while (kind < last_kind && i >= counts[kind]) {
+        i -= counts[kind];
+        kind++;
+    }
+    const RayRec r = W.q[kind][i];
+    target = (rt_asuint(r.o.w) << 3) | (uint32_t)kind;
+    return r;
 }
 
 // Short-stack form; false = stack overflow, re-run query_closest().

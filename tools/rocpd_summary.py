@@ -1,0 +1,57 @@
+"""Summaries of rocprofv3 sqlite outputs (*_results.db): per-kernel time
+(--kernel-trace) and per-kernel PMC counter totals (--pmc passes).
+
+  python tools/rocpd_summary.py trace DB          -> kernel stats table
+  python tools/rocpd_summary.py pmc DB [DB ...]   -> counters per kernel
+"""
+import sqlite3
+import sys
+from collections import defaultdict
+
+
+def short(name):
+    import re
+    m = re.search(r"k_[a-z_]+(?:<[^>]*>)?", name)
+    n = m.group(0) if m else name[:60]
+    t = re.search(r"ILb(\d)E(?:Lb(\d)E)?", name)
+    if t:
+        n += "<" + ",".join(x for x in t.groups() if x is not None) + ">"
+    return n
+
+
+def trace(db):
+    c = sqlite3.connect(db)
+    rows = c.execute("select name, end - start from kernels").fetchall()
+    agg = defaultdict(lambda: [0, 0.0, 0.0, 1e30])
+    for name, dur in rows:
+        a = agg[short(name)]
+        a[0] += 1
+        a[1] += dur
+        a[2] = max(a[2], dur)
+        a[3] = min(a[3], dur)
+    tot = sum(a[1] for a in agg.values())
+    print(f"{'kernel':40s} {'calls':>7s} {'total_ms':>10s} {'avg_us':>10s} {'min_us':>9s} {'max_us':>10s} {'pct':>6s}")
+    for k, a in sorted(agg.items(), key=lambda kv: -kv[1][1]):
+        print(f"{k:40s} {a[0]:7d} {a[1] / 1e6:10.2f} {a[1] / a[0] / 1e3:10.2f} {a[3] / 1e3:9.2f} {a[2] / 1e3:10.2f} "
+              f"{100 * a[1] / tot:6.2f}")
+
+
+def pmc(dbs):
+    agg = defaultdict(lambda: defaultdict(float))
+    for db in dbs:
+        c = sqlite3.connect(db)
+        cols = [r[1] for r in c.execute("pragma table_info(counters_collection)")]
+        q = "select kernel_name, counter_name, counter_value from counters_collection"
+        for kname, cname, val in c.execute(q):
+            agg[short(kname)][cname] += val
+    for k, d in sorted(agg.items()):
+        print(k)
+        for cn, v in sorted(d.items()):
+            print(f"   {cn:32s} {v:18.4g}")
+
+
+if __name__ == "__main__":
+    if sys.argv[1] == "trace":
+        trace(sys.argv[2])
+    else:
+        pmc(sys.argv[2:])
