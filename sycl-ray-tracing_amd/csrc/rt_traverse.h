@@ -346,7 +346,8 @@ RT_HD bool trava_step(const RtSceneView& S, TravA& T, SpillStack<FAST>& stk, Sta
         return T.mode != TM_DONE;
     }
     {
-        const uint32_t rec = T.base + T.c;
+        // children in reverse, so that child 0 is popped first (trace_any's order)
+        const uint32_t rec = T.base + (T.n - 1 - T.c);
         float tn;
         if (st) st->c[RT_STAT_ANY_VOL]++;
         if (slab_test(load_node(S.nodes, rec), T.K, tn)) {
