@@ -10,7 +10,14 @@ export TMPDIR=/tmp
 run() { # name, rocprof args...
   local name=$1; shift
   timeout -k 10 300 rocprofv3 "$@" -d "$OUT/$name" -o "$name" -- python3 bench.py $ARGS > "$OUT/$name.log" 2>&1
-  local rc=$?; echo "$name rc=$rc"; return $rc
+  local rc=$?; echo "$name rc=$rc"
+  # keep only text summaries (the sqlite files of long runs exceed what gpurun copies back)
+  for db in $(find "$OUT/$name" -name "*.db"); do
+    if [ "$name" = trace ]; then python3 tools/rocpd_summary.py trace "$db" > "$OUT/$name.summary.txt" 2>&1
+    else python3 tools/rocpd_summary.py pmc "$db" > "$OUT/$name.summary.txt" 2>&1; fi
+  done
+  rm -rf "$OUT/$name"
+  return $rc
 }
 run trace --kernel-trace --stats || exit 1
 run pmc1 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU || exit 1

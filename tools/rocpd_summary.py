@@ -41,7 +41,10 @@ def pmc(dbs):
     for db in dbs:
         c = sqlite3.connect(db)
         cols = [r[1] for r in c.execute("pragma table_info(counters_collection)")]
-        q = "select kernel_name, counter_name, counter_value from counters_collection"
+        name_col = "kernel_name" if "kernel_name" in cols else [x for x in cols if "kernel" in x and "name" in x][0]
+        cn_col = "counter_name" if "counter_name" in cols else [x for x in cols if "counter" in x and "name" in x][0]
+        val_col = [x for x in ("counter_value", "value") if x in cols][0]
+        q = f"select {name_col}, {cn_col}, {val_col} from counters_collection"
         for kname, cname, val in c.execute(q):
             agg[short(kname)][cname] += val
     for k, d in sorted(agg.items()):
