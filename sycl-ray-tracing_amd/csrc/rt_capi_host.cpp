@@ -41,6 +41,11 @@ RtSceneView rt_host_view(const rt_context* c)
     v.ew = c->ew;
     v.eh = c->eh;
     v.n_tris = (int)(c->tris.size() / 9);
+    v.chain_monotone = c->flat.chain_monotone ? 1 : 0;
+    v.bvh = c->flat.bvh.data();
+    v.bvh_tri4 = c->flat.bvh_tri4.data();
+    v.parent = c->flat.parent.data();
+    v.leaf_of = c->flat.leaf_of.data();
     return v;
 }
 
@@ -138,6 +143,7 @@ int rt_build_bvh(rt_context* c, int max_depth, int leaf_max)
     rt::build_octree(c->tris.data(), n, max_depth, leaf_max, c->octree);
     rt::flatten_octree(c->octree, c->tris.data(), n, c->flat);
     if (c->flat.max_depth > 32) return rt_fail(c, RT_ERR_ARG, "rt_build_bvh: octree deeper than 32");
+    rt::build_search_bvh(c->flat);
     c->have_bvh = true;
     c->dirty = true;
     return RT_OK;
@@ -157,6 +163,7 @@ int rt_set_bvh_preorder(rt_context* c, const void* dump, long bytes)
     c->octree = std::move(t);
     rt::flatten_octree(c->octree, c->tris.data(), n, c->flat);
     if (c->flat.max_depth > 32) return rt_fail(c, RT_ERR_ARG, "rt_set_bvh_preorder: octree deeper than 32");
+    rt::build_search_bvh(c->flat);
     c->have_bvh = true;
     c->dirty = true;
     return RT_OK;
@@ -178,7 +185,8 @@ int rt_bvh_info(const rt_context* c, long* info)
     info[2] = (long)(c->tris.size() / 9);
     info[3] = c->flat.max_depth;
     info[4] = (long)(c->flat.nodes.size() * sizeof(RtNode) + c->flat.tri4.size() * sizeof(float4_) +
-                     c->flat.prim2k.size() * 4);
+                     c->flat.prim2k.size() * 4 + c->flat.parent.size() * 4 + c->flat.leaf_of.size() * 4 +
+                     c->flat.bvh.size() * sizeof(BvhNode) + c->flat.bvh_tri4.size() * sizeof(float4_));
     return RT_OK;
 }
 

@@ -31,6 +31,17 @@ struct alignas(16) RtNode {
 };
 static_assert(sizeof(RtNode) == 64, "RtNode must be 64 B");
 
+// Search BVH (binary, SAH) over the same triangles, used to find the closest
+// Moller-Trumbore hit fast; the octree then verifies it (rt_fast.h). 64 B:
+// the two child boxes (conservatively padded) and, per child, an inner node
+// index (count 0), a leaf's first entry in bvh_tri4 (count > 0) or nothing
+// (count -1).
+struct alignas(16) BvhNode {
+    float lmin[3], lmax[3], rmin[3], rmax[3];
+    int32_t left, right, lcount, rcount;
+};
+static_assert(sizeof(BvhNode) == 64, "BvhNode must be 64 B");
+
 struct alignas(16) RtMat {
     float er, eg, eb, metalness;
     float dr, dg, db, roughness;
@@ -48,7 +59,12 @@ struct RtSceneView {
     const float* env_lum;
     const float* cdf;
     int32_t n_emissive, n_spheres, ew, eh;
-    int32_t n_tris, pad0, pad1, pad2;
+    int32_t n_tris, chain_monotone, pad1, pad2;  // chain_monotone: see rt_fast.h chain_ok
+    // search BVH + octree back-links for the verification walk
+    const BvhNode* bvh;        // [0] = root (its two boxes are the scene's halves)
+    const float4_* bvh_tri4;   // 3 records per triangle in BVH leaf order: {a.xyz, k}, {e1}, {e2}
+    const int32_t* parent;     // octree record -> parent record (-1 for the root)
+    const int32_t* leaf_of;    // leaf-order triangle k -> its octree leaf record
 };
 
 struct RtCamera {
@@ -73,5 +89,7 @@ enum {
     RT_STAT_ANY_VOL,
     RT_STAT_ANY_TRI,
     RT_STAT_ANY_LEAF,
+    RT_STAT_VERIFY,    // octree slab tests of the verification walks
+    RT_STAT_FALLBACK,  // queries answered by the exact octree walk
     RT_STAT_COUNT
 };

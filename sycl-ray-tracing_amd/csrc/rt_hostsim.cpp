@@ -20,6 +20,9 @@
 #ifndef RT_HOSTSIM_SHORT_CAP
 #define RT_HOSTSIM_SHORT_CAP 8
 #endif
+#ifndef RT_HOSTSIM_FAST_CAP
+#define RT_HOSTSIM_FAST_CAP 32
+#endif
 #ifndef RT_HOSTSIM_BUDGET
 #define RT_HOSTSIM_BUDGET 24
 #endif
@@ -86,10 +89,44 @@ static int run_wave_host(rt_context* c, int w, int h, int spp, int bounces, cons
     for (long it = 0;; it++) {
         const int par = (int)(it & 1);
         W.park_par = par;
+        // fast queries through the search BVH; failures go to the fallback lists
+        int nq = 0;
+        for (int k = rtk::RK_CONT; k <= last_kind; k++) nq += counters[k];
+        const int nqa = W.any_rays ? counters[rtk::RK_ESH] + counters[rtk::RK_BENV] : 0;
+        int fbc = 0, fba = 0;
+#pragma omp parallel
+        {
+            rtk::IdxStack<RT_HOSTSIM_FAST_CAP> fst;
+            rtk::Stats* ps = c->stats_enabled ? &st[omp_get_thread_num()] : nullptr;
+#pragma omp for schedule(dynamic, 64)
+            for (int idx = 0; idx < nq; idx++) {
+                uint32_t target;
+                rtk::RayRec r = rtk::queue_item(W, counters, rtk::RK_CONT, last_kind, idx, target);
+                float t;
+                int k;
+                if (rtk::fast_query_closest(W.S, rtk::v3of(r.o), rtk::v3of(r.d), fst, t, k, ps)) {
+                    rtk::finish_closest(W, target, rtk::v3of(r.o), rtk::v3of(r.d), t, k);
+                } else {
+                    r.d.w = rt_asfloat(target & 7u);
+                    W.fb_c[__atomic_fetch_add(&fbc, 1, __ATOMIC_RELAXED)] = r;
+                }
+            }
+#pragma omp for schedule(dynamic, 64)
+            for (int idx = 0; idx < nqa; idx++) {
+                uint32_t target;
+                rtk::RayRec r = rtk::queue_item(W, counters, rtk::RK_ESH, rtk::RK_BENV, idx, target);
+                const int a = rtk::fast_query_any(W.S, rtk::v3of(r.o), rtk::v3of(r.d), fst, ps);
+                if (a >= 0) {
+                    rtk::finish_any(W, target, a == 1);
+                } else {
+                    r.d.w = rt_asfloat(target & 7u);
+                    W.fb_a[__atomic_fetch_add(&fba, 1, __ATOMIC_RELAXED)] = r;
+                }
+            }
+        }
+        // exact walks: parked queries, then the fallback lists
         const int nrc = std::min(parkc[par], W.park_cap), nra = std::min(parka[par], W.park_cap);
-        int nc = nrc, na = nra;
-        for (int k = rtk::RK_CONT; k <= last_kind; k++) nc += counters[k];
-        if (W.any_rays) na += counters[rtk::RK_ESH] + counters[rtk::RK_BENV];
+        const int nc = nrc + fbc, na = nra + fba;
 #pragma omp parallel
         {
             std::vector<uint32_t> spr(RT_STACK_CAP);
@@ -105,7 +142,9 @@ static int run_wave_host(rt_context* c, int w, int h, int spp, int bounces, cons
                     target = rtk::travc_resume(&W.park_c[par][idx], T, stk);
                     has = true;
                 } else {
-                    const rtk::RayRec r = rtk::queue_item(W, counters, rtk::RK_CONT, last_kind, idx - nrc, target);
+                    const rtk::RayRec r = W.fb_c[idx - nrc];
+                    target = (rt_asuint(r.o.w) << 3) | rt_asuint(r.d.w);
+                    if (ps) ps->c[RT_STAT_FALLBACK]++;
                     has = rtk::travc_begin(W.S, T, rtk::v3of(r.o), rtk::v3of(r.d), ps);
                     if (!has) rtk::finish_closest(W, target, T.o, T.d, T.best_t, T.best_k);
                 }
@@ -135,7 +174,9 @@ static int run_wave_host(rt_context* c, int w, int h, int spp, int bounces, cons
                     target = rtk::trava_resume(&W.park_a[par][idx], T, stk);
                     has = true;
                 } else {
-                    const rtk::RayRec r = rtk::queue_item(W, counters, rtk::RK_ESH, rtk::RK_BENV, idx - nra, target);
+                    const rtk::RayRec r = W.fb_a[idx - nra];
+                    target = (rt_asuint(r.o.w) << 3) | rt_asuint(r.d.w);
+                    if (ps) ps->c[RT_STAT_FALLBACK]++;
                     has = rtk::trava_begin(W.S, T, rtk::v3of(r.o), rtk::v3of(r.d), ps);
                     if (!has) rtk::finish_any(W, target, false);
                 }

@@ -45,6 +45,10 @@ enum {
     C_TK_CLOSEST = rtk::RK_COUNT,
     C_TK_ANY,
     C_TK_STEP,
+    C_TK_EXACT_C,             // tickets of the exact (fallback) kernels
+    C_TK_EXACT_A,
+    C_FBC,                    // fallback list sizes
+    C_FBA,
     C_ACT0,                   // live-slot counts, double-buffered
     C_ACT1,
     C_PARKC0,                 // parked queries, double-buffered by iteration parity
@@ -56,6 +60,7 @@ enum {
 
 struct Backend {
     DevBuf nodes, tri4, prim2k, mat_idx, mats, emissive, spheres, env, env_lum, cdf;
+    DevBuf bvh, bvh_tri4, parent, leaf_of;
     DevBuf stats;     // RT_STAT_COUNT u64
     DevBuf wave;      // path state, pending records, results, queues, lists
     DevBuf counters;  // C_COUNT int32
@@ -200,7 +205,91 @@ __global__ __launch_bounds__(256) void k_step(rtk::WaveView W, const int32_t* ac
     flush_stats<STATS>(st, stats);
 }
 
-// ------------------------------------------------------------- trace kernels
+// -------------------------------------------------------- fast query kernels
+// One query per lane at a time through the search BVH (rt_fast.h), stack of
+// node indices in LDS; a query whose answer needs the exact octree walk (or
+// whose stack would overflow) goes to the fallback list for
+// k_exact_closest / k_exact_any.
+#define RT_LDS_CAP_FAST 32
+
+template <int N>
+struct LdsIdx {
+    static constexpr int CAP = N;
+    uint32_t* r;
+    __device__ __forceinline__ uint32_t rec(int i) const { return r[i * 256]; }
+    __device__ __forceinline__ void set_rec(int i, uint32_t v) { r[i * 256] = v; }
+};
+
+template <bool STATS>
+__global__ __launch_bounds__(256) void k_fast_closest(rtk::WaveView W, unsigned long long* stats)
+{
+    __shared__ uint32_t s_r[RT_LDS_CAP_FAST * 256];
+    LdsIdx<RT_LDS_CAP_FAST> stk{s_r + threadIdx.x};
+    const int last_kind = W.any_rays ? rtk::RK_BL : rtk::RK_BENV;
+    int total = 0;
+    for (int k = rtk::RK_CONT; k <= last_kind; k++) total += W.counters[C_Q0 + k];
+    rtk::Stats st;
+    if (STATS)
+        for (int i = 0; i < RT_STAT_COUNT; i++) st.c[i] = 0;
+    for (;;) {
+        const int base = wave_ticket(W.counters + C_TK_CLOSEST);
+        if (base >= total) break;
+        const int idx = base + lane_id();
+        bool fail = false;
+        rtk::RayRec r;
+        uint32_t target = 0;
+        if (idx < total) {
+            r = rtk::queue_item(W, W.counters + C_Q0, rtk::RK_CONT, last_kind, idx, target);
+            float t;
+            int k;
+            if (rtk::fast_query_closest(W.S, rtk::v3of(r.o), rtk::v3of(r.d), stk, t, k, STATS ? &st : nullptr))
+                rtk::finish_closest(W, target, rtk::v3of(r.o), rtk::v3of(r.d), t, k);
+            else
+                fail = true;
+        }
+        const int f = wave_append(W.counters + C_FBC, fail);
+        if (fail) {
+            r.d.w = rt_asfloat(target & 7u);
+            W.fb_c[f] = r;
+        }
+    }
+    flush_stats<STATS>(st, stats);
+}
+
+template <bool STATS>
+__global__ __launch_bounds__(256) void k_fast_any(rtk::WaveView W, unsigned long long* stats)
+{
+    __shared__ uint32_t s_r[RT_LDS_CAP_FAST * 256];
+    LdsIdx<RT_LDS_CAP_FAST> stk{s_r + threadIdx.x};
+    const int total = W.counters[C_Q0 + rtk::RK_ESH] + W.counters[C_Q0 + rtk::RK_BENV];
+    rtk::Stats st;
+    if (STATS)
+        for (int i = 0; i < RT_STAT_COUNT; i++) st.c[i] = 0;
+    for (;;) {
+        const int base = wave_ticket(W.counters + C_TK_ANY);
+        if (base >= total) break;
+        const int idx = base + lane_id();
+        bool fail = false;
+        rtk::RayRec r;
+        uint32_t target = 0;
+        if (idx < total) {
+            r = rtk::queue_item(W, W.counters + C_Q0, rtk::RK_ESH, rtk::RK_BENV, idx, target);
+            const int a = rtk::fast_query_any(W.S, rtk::v3of(r.o), rtk::v3of(r.d), stk, STATS ? &st : nullptr);
+            if (a >= 0)
+                rtk::finish_any(W, target, a == 1);
+            else
+                fail = true;
+        }
+        const int f = wave_append(W.counters + C_FBA, fail);
+        if (fail) {
+            r.d.w = rt_asfloat(target & 7u);
+            W.fb_a[f] = r;
+        }
+    }
+    flush_stats<STATS>(st, stats);
+}
+
+// ------------------------------------------------------- exact (fallback) kernels
 // Persistent waves; each lane runs one query at a time, one unit of work per
 // loop trip (rt_traverse.h). Idle lanes refill from the work list (parked
 // queries of the last launch first, then the queues) once REFILL lanes are
@@ -209,7 +298,7 @@ __global__ __launch_bounds__(256) void k_step(rtk::WaveView W, const int32_t* ac
 #define RT_REFILL 16
 
 template <bool STATS>
-__global__ __launch_bounds__(256, 4) void k_trace_closest(rtk::WaveView W, unsigned long long* stats)
+__global__ __launch_bounds__(256, 4) void k_exact_closest(rtk::WaveView W, unsigned long long* stats)
 {
     __shared__ uint32_t s_r[RT_LDS_CAP_CLOSEST * 256];
     __shared__ float s_k[RT_LDS_CAP_CLOSEST * 256];
@@ -219,9 +308,7 @@ __global__ __launch_bounds__(256, 4) void k_trace_closest(rtk::WaveView W, unsig
                               W.spill_k + (size_t)gl * RT_STACK_CAP};
     const int par = W.park_par;
     const int n_res = min(W.counters[C_PARKC0 + par], W.park_cap);
-    const int last_kind = W.any_rays ? rtk::RK_BL : rtk::RK_BENV;
-    int total = n_res;
-    for (int k = rtk::RK_CONT; k <= last_kind; k++) total += W.counters[C_Q0 + k];
+    const int total = n_res + W.counters[C_FBC];
     rtk::Stats st;
     if (STATS)
         for (int i = 0; i < RT_STAT_COUNT; i++) st.c[i] = 0;
@@ -234,7 +321,7 @@ __global__ __launch_bounds__(256, 4) void k_trace_closest(rtk::WaveView W, unsig
         const int nneed = __popcll(bneed);
         if (!drained && (nneed >= RT_REFILL || nneed == 64)) {
             int base = 0;
-            if (lane_id() == 0) base = atomicAdd(W.counters + C_TK_CLOSEST, nneed);
+            if (lane_id() == 0) base = atomicAdd(W.counters + C_TK_EXACT_C, nneed);
             base = __shfl(base, 0);
             if (base + nneed >= total) drained = true;
             if (need) {
@@ -243,9 +330,10 @@ __global__ __launch_bounds__(256, 4) void k_trace_closest(rtk::WaveView W, unsig
                     target = rtk::travc_resume(&W.park_c[par][idx], T, stk);
                     has = resumed = true;
                 } else if (idx < total) {
-                    const rtk::RayRec r = rtk::queue_item(W, W.counters + C_Q0, rtk::RK_CONT, last_kind, idx - n_res,
-                                                          target);
+                    const rtk::RayRec r = W.fb_c[idx - n_res];
+                    target = (rt_asuint(r.o.w) << 3) | rt_asuint(r.d.w);
                     resumed = false;
+                    if (STATS) st.c[RT_STAT_FALLBACK]++;
                     has = rtk::travc_begin(W.S, T, rtk::v3of(r.o), rtk::v3of(r.d), STATS ? &st : nullptr);
                     if (!has) rtk::finish_closest(W, target, T.o, T.d, T.best_t, T.best_k);
                 }
@@ -276,7 +364,7 @@ __global__ __launch_bounds__(256, 4) void k_trace_closest(rtk::WaveView W, unsig
 }
 
 template <bool STATS>
-__global__ __launch_bounds__(256, 4) void k_trace_any(rtk::WaveView W, unsigned long long* stats)
+__global__ __launch_bounds__(256, 4) void k_exact_any(rtk::WaveView W, unsigned long long* stats)
 {
     __shared__ uint32_t s_r[RT_LDS_CAP_ANY * 256];
     using FAST = LdsStack<RT_LDS_CAP_ANY>;
@@ -284,7 +372,7 @@ __global__ __launch_bounds__(256, 4) void k_trace_any(rtk::WaveView W, unsigned 
     rtk::SpillStack<FAST> stk{FAST{s_r + threadIdx.x, nullptr}, W.spill_r + (size_t)gl * RT_STACK_CAP, nullptr};
     const int par = W.park_par;
     const int n_res = min(W.counters[C_PARKA0 + par], W.park_cap);
-    const int total = n_res + W.counters[C_Q0 + rtk::RK_ESH] + W.counters[C_Q0 + rtk::RK_BENV];
+    const int total = n_res + W.counters[C_FBA];
     rtk::Stats st;
     if (STATS)
         for (int i = 0; i < RT_STAT_COUNT; i++) st.c[i] = 0;
@@ -297,7 +385,7 @@ __global__ __launch_bounds__(256, 4) void k_trace_any(rtk::WaveView W, unsigned 
         const int nneed = __popcll(bneed);
         if (!drained && (nneed >= RT_REFILL || nneed == 64)) {
             int base = 0;
-            if (lane_id() == 0) base = atomicAdd(W.counters + C_TK_ANY, nneed);
+            if (lane_id() == 0) base = atomicAdd(W.counters + C_TK_EXACT_A, nneed);
             base = __shfl(base, 0);
             if (base + nneed >= total) drained = true;
             if (need) {
@@ -306,9 +394,10 @@ __global__ __launch_bounds__(256, 4) void k_trace_any(rtk::WaveView W, unsigned 
                     target = rtk::trava_resume(&W.park_a[par][idx], T, stk);
                     has = resumed = true;
                 } else if (idx < total) {
-                    const rtk::RayRec r = rtk::queue_item(W, W.counters + C_Q0, rtk::RK_ESH, rtk::RK_BENV,
-                                                          idx - n_res, target);
+                    const rtk::RayRec r = W.fb_a[idx - n_res];
+                    target = (rt_asuint(r.o.w) << 3) | rt_asuint(r.d.w);
                     resumed = false;
+                    if (STATS) st.c[RT_STAT_FALLBACK]++;
                     has = rtk::trava_begin(W.S, T, rtk::v3of(r.o), rtk::v3of(r.d), STATS ? &st : nullptr);
                     if (!has) rtk::finish_any(W, target, false);
                 }
@@ -428,7 +517,8 @@ void rt_backend_destroy(rt_context* c)
     if (!b) return;
     (void)hipSetDevice(c->device);
     DevBuf* all[] = {&b->nodes, &b->tri4, &b->prim2k, &b->mat_idx, &b->mats, &b->emissive, &b->spheres, &b->env,
-                     &b->env_lum, &b->cdf, &b->stats, &b->wave, &b->counters, &b->xy, &b->fb};
+                     &b->env_lum, &b->cdf, &b->bvh, &b->bvh_tri4, &b->parent, &b->leaf_of, &b->stats, &b->wave,
+                     &b->counters, &b->xy, &b->fb};
     for (DevBuf* d : all)
         if (d->p) (void)hipFree(d->p);
     if (b->h_act) (void)hipHostFree(b->h_act);
@@ -451,6 +541,8 @@ int rt_backend_upload(rt_context* c)
         (r = upload(c, b->mats, c->mats)) || (r = upload(c, b->emissive, c->emissive)) ||
         (r = upload(c, b->spheres, c->spheres)) || (r = upload(c, b->env, c->env)) ||
         (r = upload(c, b->env_lum, c->env_lum)) || (r = upload(c, b->cdf, c->cdf)) ||
+        (r = upload(c, b->bvh, c->flat.bvh)) || (r = upload(c, b->bvh_tri4, c->flat.bvh_tri4)) ||
+        (r = upload(c, b->parent, c->flat.parent)) || (r = upload(c, b->leaf_of, c->flat.leaf_of)) ||
         (r = ensure(c, b->stats, RT_STAT_COUNT * sizeof(unsigned long long))) ||
         (r = ensure(c, b->counters, C_COUNT * sizeof(int32_t))))
         return r;
@@ -470,6 +562,11 @@ int rt_backend_upload(rt_context* c)
     v.ew = c->ew;
     v.eh = c->eh;
     v.n_tris = (int)(c->tris.size() / 9);
+    v.chain_monotone = c->flat.chain_monotone ? 1 : 0;
+    v.bvh = (const BvhNode*)b->bvh.p;
+    v.bvh_tri4 = (const float4_*)b->bvh_tri4.p;
+    v.parent = (const int32_t*)b->parent.p;
+    v.leaf_of = (const int32_t*)b->leaf_of.p;
     b->view = v;
     b->bl_rays = rt_scene_has_emissive_prim(c) ? 1 : 0;
     b->any_rays = v.n_spheres == 0 ? 1 : 0;
@@ -485,7 +582,8 @@ static int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounce
     (void)hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, c->device);
     const int threads = 256;
     const int step_blocks = std::min((n + threads - 1) / threads, dev_cus * 8);
-    const int trace_blocks = dev_cus * 4;  // persistent: 4 blocks of 256 per CU (LDS stacks, 4 waves/SIMD)
+    const int trace_blocks = dev_cus * 4;  // exact kernels: persistent, 4 blocks of 256 per CU
+    const int fast_blocks = dev_cus * 4;   // fast kernels: persistent (LDS stack 32 KB per block)
     rtk::WaveView W{};
     W.park_cap = 1 << 16;
     W.spill_lanes = trace_blocks * threads;
@@ -534,16 +632,22 @@ static int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounce
                 if (!b->tev[k][it]) HIPCHK(c, hipEventCreate(&b->tev[k][it]));
         W.park_par = cur;
         if (T) HIPCHK(c, hipEventRecord(b->tev[0][it], s));
-        if (S)
-            hipLaunchKernelGGL(k_trace_closest<true>, dim3(trace_blocks), dim3(threads), 0, s, W, stats);
-        else
-            hipLaunchKernelGGL(k_trace_closest<false>, dim3(trace_blocks), dim3(threads), 0, s, W, stats);
+        if (S) {
+            hipLaunchKernelGGL(k_fast_closest<true>, dim3(fast_blocks), dim3(threads), 0, s, W, stats);
+            hipLaunchKernelGGL(k_exact_closest<true>, dim3(trace_blocks), dim3(threads), 0, s, W, stats);
+        } else {
+            hipLaunchKernelGGL(k_fast_closest<false>, dim3(fast_blocks), dim3(threads), 0, s, W, stats);
+            hipLaunchKernelGGL(k_exact_closest<false>, dim3(trace_blocks), dim3(threads), 0, s, W, stats);
+        }
         if (T) HIPCHK(c, hipEventRecord(b->tev[1][it], s));
         if (W.any_rays) {
-            if (S)
-                hipLaunchKernelGGL(k_trace_any<true>, dim3(trace_blocks), dim3(threads), 0, s, W, stats);
-            else
-                hipLaunchKernelGGL(k_trace_any<false>, dim3(trace_blocks), dim3(threads), 0, s, W, stats);
+            if (S) {
+                hipLaunchKernelGGL(k_fast_any<true>, dim3(fast_blocks), dim3(threads), 0, s, W, stats);
+                hipLaunchKernelGGL(k_exact_any<true>, dim3(trace_blocks), dim3(threads), 0, s, W, stats);
+            } else {
+                hipLaunchKernelGGL(k_fast_any<false>, dim3(fast_blocks), dim3(threads), 0, s, W, stats);
+                hipLaunchKernelGGL(k_exact_any<false>, dim3(trace_blocks), dim3(threads), 0, s, W, stats);
+            }
         }
         if (T) HIPCHK(c, hipEventRecord(b->tev[2][it], s));
         hipLaunchKernelGGL(k_reset, dim3(1), dim3(64), 0, s, cnt, C_ACT0 + (cur ^ 1), cur);

@@ -434,6 +434,8 @@ void flatten_octree(const Octree& t, const float* tris, int ntris, FlatBvh& out)
 {
     out.nodes.clear();
     out.tri4.clear();
+    out.parent.clear();
+    out.leaf_of.clear();
     out.prim2k.assign(ntris, -1);
     out.max_depth = 0;
     auto empty = [&](int ni) { return t.pool[ni].leaf && t.pool[ni].tris.empty(); };
@@ -449,6 +451,7 @@ void flatten_octree(const Octree& t, const float* tris, int ntris, FlatBvh& out)
         int ni, rec, depth;
     };
     out.nodes.push_back(RtNode{});
+    out.parent.push_back(-1);
     fill(out.nodes[0], 0);
     std::vector<Item> st{{0, 0, 0}};
     while (!st.empty()) {
@@ -460,6 +463,7 @@ void flatten_octree(const Octree& t, const float* tris, int ntris, FlatBvh& out)
             out.nodes[it.rec].ref = (uint32_t)(out.tri4.size() / 3);
             out.nodes[it.rec].cnt = RT_LEAF_BIT | (uint32_t)n.tris.size();
             for (int id : n.tris) {
+                out.leaf_of.push_back(it.rec);
                 const float* a = tris + 9 * (size_t)id;
                 float4_ r0{a[0], a[1], a[2], 0.0f}, r1{a[3] - a[0], a[4] - a[1], a[5] - a[2], 0.0f},
                     r2{a[6] - a[0], a[7] - a[1], a[8] - a[2], 0.0f};
@@ -478,8 +482,209 @@ void flatten_octree(const Octree& t, const float* tris, int ntris, FlatBvh& out)
         out.nodes[it.rec].ref = (uint32_t)base;
         out.nodes[it.rec].cnt = (uint32_t)nk;
         out.nodes.resize(base + nk);
+        out.parent.resize(base + nk, it.rec);
         for (int k = 0; k < nk; k++) fill(out.nodes[base + k], kids[k]);
         for (int k = nk - 1; k >= 0; k--) st.push_back({kids[k], base + k, it.depth + 1});
+    }
+}
+
+// ============================================================ search BVH
+namespace {
+struct Box {
+    float mn[3], mx[3];
+    void reset()
+    {
+        for (int i = 0; i < 3; i++) mn[i] = INFINITY, mx[i] = -INFINITY;
+    }
+    void grow(const float* p)
+    {
+        for (int i = 0; i < 3; i++) mn[i] = std::min(mn[i], p[i]), mx[i] = std::max(mx[i], p[i]);
+    }
+    void grow(const Box& b)
+    {
+        for (int i = 0; i < 3; i++) mn[i] = std::min(mn[i], b.mn[i]), mx[i] = std::max(mx[i], b.mx[i]);
+    }
+    float area() const
+    {
+        if (!(mx[0] >= mn[0])) return 0.0f;
+        const float dx = mx[0] - mn[0], dy = mx[1] - mn[1], dz = mx[2] - mn[2];
+        return 2.0f * (dx * dy + dy * dz + dz * dx);
+    }
+};
+struct Prim {
+    Box b;
+    float c[3];
+    int k;
+};
+constexpr int kBins = 16, kLeafMax = 4;
+
+// Pads a box so every point the reference's Moller-Trumbore test can accept
+// for its triangles (barycentric / t round-off ~1e-6 relative to coordinate
+// magnitudes) is strictly inside, and the traversal's float slab test on the
+// padded box cannot miss such a point.
+void pad_box(const Box& b, float* mn, float* mx)
+{
+    float mag = 1.0f;
+    for (int i = 0; i < 3; i++) mag = std::max(mag, std::max(std::fabs(b.mn[i]), std::fabs(b.mx[i])));
+    const float pad = 1e-4f * mag;
+    for (int i = 0; i < 3; i++) mn[i] = b.mn[i] - pad, mx[i] = b.mx[i] + pad;
+}
+
+struct SahBuilder {
+    std::vector<Prim>& P;
+    std::vector<BvhNode>& nodes;
+    std::vector<int32_t> order;  // leaf order of P indices
+    explicit SahBuilder(std::vector<Prim>& p, std::vector<BvhNode>& n) : P(p), nodes(n) {}
+
+    // Splits [b, e) in place; returns the split point or -1 for a leaf.
+    int split(int b, int e, const Box& cb)
+    {
+        const int n = e - b;
+        if (n <= kLeafMax) return -1;
+        float best = INFINITY;
+        int best_axis = -1, best_bin = -1;
+        for (int ax = 0; ax < 3; ax++) {
+            const float lo = cb.mn[ax], ext = cb.mx[ax] - cb.mn[ax];
+            if (!(ext > 0.0f)) continue;
+            Box bb[kBins];
+            int cnt[kBins] = {0};
+            for (auto& x : bb) x.reset();
+            const float sc = kBins / ext;
+            for (int i = b; i < e; i++) {
+                int bi = std::min(kBins - 1, (int)((P[i].c[ax] - lo) * sc));
+                cnt[bi]++;
+                bb[bi].grow(P[i].b);
+            }
+            float rarea[kBins];
+            int rcnt[kBins];
+            Box acc;
+            acc.reset();
+            int ac = 0;
+            for (int i = kBins - 1; i > 0; i--) {
+                acc.grow(bb[i]);
+                ac += cnt[i];
+                rarea[i] = acc.area();
+                rcnt[i] = ac;
+            }
+            acc.reset();
+            ac = 0;
+            for (int i = 0; i < kBins - 1; i++) {
+                acc.grow(bb[i]);
+                ac += cnt[i];
+                if (ac == 0 || rcnt[i + 1] == 0) continue;
+                const float cost = acc.area() * ac + rarea[i + 1] * rcnt[i + 1];
+                if (cost < best) best = cost, best_axis = ax, best_bin = i;
+            }
+        }
+        int mid;
+        if (best_axis < 0) {
+            mid = b + n / 2;  // all centroids coincide: split by count
+        } else {
+            const float lo = cb.mn[best_axis], sc = kBins / (cb.mx[best_axis] - cb.mn[best_axis]);
+            auto it = std::partition(P.begin() + b, P.begin() + e, [&](const Prim& p) {
+                return std::min(kBins - 1, (int)((p.c[best_axis] - lo) * sc)) <= best_bin;
+            });
+            mid = (int)(it - P.begin());
+            if (mid == b || mid == e) mid = b + n / 2;
+        }
+        return mid;
+    }
+
+    void run()
+    {
+        const int n = (int)P.size();
+        struct Task {
+            int b, e, node, side;  // side: 0 left child slot, 1 right child slot of `node`
+        };
+        nodes.clear();
+        nodes.push_back(BvhNode{});
+        std::vector<Task> st;
+        auto bounds = [&](int b, int e, Box& bb, Box& cb) {
+            bb.reset();
+            cb.reset();
+            for (int i = b; i < e; i++) bb.grow(P[i].b), cb.grow(P[i].c);
+        };
+        // root: split the whole set into the root node's two children
+        Box bb, cb;
+        bounds(0, n, bb, cb);
+        int mid = n > 1 ? split(0, n, cb) : -1;
+        if (mid < 0) mid = n;  // tiny scene: one leaf in the left slot, empty right
+        st.push_back({mid, n, 0, 1});
+        st.push_back({0, mid, 0, 0});
+        while (!st.empty()) {
+            const Task t = st.back();
+            st.pop_back();
+            BvhNode& parent = nodes[t.node];
+            float* mn = t.side ? parent.rmin : parent.lmin;
+            float* mx = t.side ? parent.rmax : parent.lmax;
+            int32_t& ref = t.side ? parent.right : parent.left;
+            int32_t& cnt = t.side ? parent.rcount : parent.lcount;
+            if (t.e <= t.b) {  // empty slot (count -1): never entered
+                for (int i = 0; i < 3; i++) mn[i] = INFINITY, mx[i] = -INFINITY;
+                ref = 0;
+                cnt = -1;
+                continue;
+            }
+            bounds(t.b, t.e, bb, cb);
+            pad_box(bb, mn, mx);
+            const int m = split(t.b, t.e, cb);
+            if (m < 0) {
+                ref = t.b;  // leaf entries are P[t.b .. t.e) in final order
+                cnt = t.e - t.b;
+                continue;
+            }
+            const int ni = (int)nodes.size();
+            ref = ni;
+            cnt = 0;
+            nodes.push_back(BvhNode{});  // (invalidates `parent`; not used below)
+            st.push_back({m, t.e, ni, 1});
+            st.push_back({t.b, m, ni, 0});
+        }
+    }
+};
+}  // namespace
+
+void build_search_bvh(FlatBvh& out)
+{
+    // plane nesting along every parent link (enables rt_fast.h's one-test chain check)
+    out.chain_monotone = true;
+    for (size_t r = 1; r < out.nodes.size() && out.chain_monotone; r++) {
+        const RtNode& c = out.nodes[r];
+        const RtNode& p = out.nodes[out.parent[r]];
+        for (int i = 0; i < 7; i++)
+            if (!(p.dn[i] <= c.dn[i] && p.df[i] >= c.df[i])) out.chain_monotone = false;
+    }
+    const int n = (int)(out.tri4.size() / 3);
+    std::vector<Prim> P(n);
+    for (int k = 0; k < n; k++) {
+        const float4_* r = &out.tri4[3 * (size_t)k];
+        const float a[3] = {r[0].x, r[0].y, r[0].z};
+        // vertices as the reference's Triangle holds them: b = a + e1, c = a + e2
+        // may differ from the originals in the last ulp; pad_box absorbs it.
+        const float b[3] = {r[0].x + r[1].x, r[0].y + r[1].y, r[0].z + r[1].z};
+        const float c[3] = {r[0].x + r[2].x, r[0].y + r[2].y, r[0].z + r[2].z};
+        P[k].b.reset();
+        P[k].b.grow(a);
+        P[k].b.grow(b);
+        P[k].b.grow(c);
+        for (int i = 0; i < 3; i++) P[k].c[i] = 0.5f * (P[k].b.mn[i] + P[k].b.mx[i]);
+        P[k].k = k;
+    }
+    SahBuilder B(P, out.bvh);
+    if (n > 0) B.run();
+    out.bvh_tri4.resize(3 * (size_t)n);
+    for (int i = 0; i < n; i++) {
+        const int k = P[i].k;
+        out.bvh_tri4[3 * (size_t)i] = out.tri4[3 * (size_t)k];
+        std::memcpy(&out.bvh_tri4[3 * (size_t)i].w, &k, 4);
+        out.bvh_tri4[3 * (size_t)i + 1] = out.tri4[3 * (size_t)k + 1];
+        out.bvh_tri4[3 * (size_t)i + 2] = out.tri4[3 * (size_t)k + 2];
+    }
+    if (out.bvh.empty()) {  // no triangles: a root with two empty slots
+        BvhNode r{};
+        for (int i = 0; i < 3; i++) r.lmin[i] = r.rmin[i] = INFINITY, r.lmax[i] = r.rmax[i] = -INFINITY;
+        r.lcount = r.rcount = -1;
+        out.bvh.push_back(r);
     }
 }
 

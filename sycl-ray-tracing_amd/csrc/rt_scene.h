@@ -56,9 +56,19 @@ struct FlatBvh {
     std::vector<RtNode> nodes;    // nodes[0] = root record
     std::vector<float4_> tri4;    // 3 records per triangle, leaf order
     std::vector<int32_t> prim2k;  // triangle id -> leaf-order index
+    std::vector<int32_t> parent;  // record -> parent record (-1: root)
+    std::vector<int32_t> leaf_of; // leaf-order index k -> leaf record
     int max_depth = 0;            // deepest non-empty node
+    bool chain_monotone = false;  // every record's planes lie within its parent's
+    // search BVH over tri4 (build_search_bvh)
+    std::vector<BvhNode> bvh;
+    std::vector<float4_> bvh_tri4;
 };
 void flatten_octree(const Octree& t, const float* tris, int ntris, FlatBvh& out);
+// Binned-SAH binary BVH over out.tri4 (leaf size <= 4), boxes padded so that
+// any triangle the reference's Moller-Trumbore test reports as hit lies in
+// the boxes the traversal enters.
+void build_search_bvh(FlatBvh& out);
 
 // ------------------------------------------------------------------ env
 // lum[i] = (float)(0.3086*r + 0.6094*g + 0.0820*b) in double (image.h:80-85)

@@ -20,7 +20,7 @@
 // the launch's pixel source): 16-B records so a wave's loads coalesce.
 #pragma once
 
-#include "rt_traverse.h"
+#include "rt_fast.h"
 
 namespace rtk {
 
@@ -98,6 +98,8 @@ struct WaveView {
     RayRec* q[RK_COUNT];    // [n_slots] each
     int32_t* counters;      // queue sizes, tickets, live counts (rt_render.hip C_*)
     int32_t* r_park;        // [n_slots] queries of the slot parked (the step skips the slot while > 0)
+    RayRec* fb_c;           // [5 n_slots] closest-hit queries left to the exact walk (d.w = kind)
+    RayRec* fb_a;           // [2 n_slots] occlusion queries left to the exact walk
     ParkC* park_c[2];       // parked closest-hit queries, double-buffered by iteration parity
     ParkA* park_a[2];
     int park_cap;
@@ -146,6 +148,8 @@ inline size_t wave_carve(char* base, size_t n, WaveView& W)  // uses W.park_cap,
     W.act_in = (const int32_t*)take(n * 4);
     W.act_out = (int32_t*)take(n * 4);
     W.r_park = (int32_t*)take(n * 4);
+    W.fb_c = (RayRec*)take(5 * n * sizeof(RayRec));
+    W.fb_a = (RayRec*)take(2 * n * sizeof(RayRec));
     for (int k = 0; k < 2; k++) {
         W.park_c[k] = (ParkC*)take((size_t)W.park_cap * sizeof(ParkC));
         W.park_a[k] = (ParkA*)take((size_t)W.park_cap * sizeof(ParkA));

@@ -66,7 +66,7 @@ _SIGS = {
 }
 
 STAT_NAMES = ["rays", "vol", "tri", "leaf", "mat", "env", "cdf", "heap_slow", "any_rays", "any_vol", "any_tri",
-              "any_leaf"]
+              "any_leaf", "verify", "fallback"]
 
 _libs: dict = {}
 
