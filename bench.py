@@ -47,18 +47,22 @@ CONFIGS = {
     "cfg2s": ("dragon", "L", "dragon", 480, 270, 16, 8, "profiling-sized cfg2: dragon 480x270x16spp x8"),
 }
 HBM_PEAK_GBS = 8000.0  # /opt/skills/guides/MI355X_MICROARCH.md (spec)
-# SURVEY.md §8(d) byte model: per child-volume test 56 B (7+7 f32 planes),
-# per triangle test 36 B (3 vertices), per material fetch 40 B, per env
-# texel 16 B, per CDF probe 4 B. The dominant kernel is the closest-hit
-# trace; its algorithmic bytes are its own volume and triangle tests.
-BYTES = {"vol": 56, "tri": 36, "mat": 40, "env": 16, "cdf": 4}
+# Algorithmic bytes per unit of work: the records a query
+# must read. Search-BVH box test 32 B (half of a 64-B node), triangle test
+# 48 B (a, e1, e2 as 3 x 16 B), octree verification slab test 64 B (one
+# record), queue ray 32 B + result 8 B per query; step kernel: material
+# 32 B, env texel 16 B, CDF probe 4 B. (SURVEY.md §8(d)'s model of the
+# reference's own octree walk — 56 B per child volume, 36 B per triangle —
+# is reported beside it as `ref_model_bytes_per_sample`.)
+BYTES = {"box": 32, "tri": 48, "verify": 64, "ray": 40, "mat": 32, "env": 16, "cdf": 4}
 
 
 def algo_bytes(st: dict, kernel: str) -> float:
     if kernel == "trace_closest":
-        return BYTES["vol"] * st["vol"] + BYTES["tri"] * st["tri"]
+        return (BYTES["box"] * st["vol"] + BYTES["tri"] * st["tri"] + BYTES["verify"] * st["verify"] +
+                BYTES["ray"] * st["rays"])
     if kernel == "trace_any":
-        return BYTES["vol"] * st["any_vol"] + BYTES["tri"] * st["any_tri"]
+        return BYTES["box"] * st["any_vol"] + BYTES["tri"] * st["any_tri"] + BYTES["ray"] * st["any_rays"]
     return BYTES["mat"] * st["mat"] + BYTES["env"] * st["env"] + BYTES["cdf"] * st["cdf"]
 
 
