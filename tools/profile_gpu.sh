@@ -14,12 +14,14 @@ run() { # name, rocprof args...
   # keep only text summaries (the sqlite files of long runs exceed what gpurun copies back)
   for db in $(find "$OUT/$name" -name "*.db"); do
     if [ "$name" = trace ]; then python3 tools/rocpd_summary.py trace "$db" > "$OUT/$name.summary.txt" 2>&1
-    else python3 tools/rocpd_summary.py pmc "$db" > "$OUT/$name.summary.txt" 2>&1; fi
+    else python3 tools/rocpd_summary.py pmc "$db" > "$OUT/$name.summary.txt" 2>&1
+         python3 tools/rocpd_summary.py pmcjson "$OUT/$name.json" "$db" > /dev/null 2>&1; fi
   done
+  for f in $(find "$OUT/$name" -name "*kernel_stats.csv"); do cp "$f" "$OUT/$name.kernel_stats.csv"; done
   rm -rf "$OUT/$name"
   return $rc
 }
-run trace --kernel-trace --stats || exit 1
+run trace --kernel-trace --stats --output-format csv rocpd || exit 1
 run pmc1 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU || exit 1
 run pmc2 --pmc SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_SALU SQ_INST_CYCLES_VMEM_RD SQ_THREAD_CYCLES_VALU SQ_LEVEL_WAVES SQ_INSTS_VALU_FLOPS_FP64 SQ_LDS_BANK_CONFLICT || exit 1
 run pmc3 --pmc TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum GRBM_GUI_ACTIVE TCP_PENDING_STALL_CYCLES_sum || exit 1

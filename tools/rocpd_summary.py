@@ -36,19 +36,26 @@ def trace(db):
               f"{100 * a[1] / tot:6.2f}")
 
 
-def pmc(dbs):
+def pmc(dbs, as_json=None):
     agg = defaultdict(lambda: defaultdict(float))
+    disp = defaultdict(set)
     for db in dbs:
         c = sqlite3.connect(db)
         cols = [r[1] for r in c.execute("pragma table_info(counters_collection)")]
         name_col = "kernel_name" if "kernel_name" in cols else [x for x in cols if "kernel" in x and "name" in x][0]
         cn_col = "counter_name" if "counter_name" in cols else [x for x in cols if "counter" in x and "name" in x][0]
         val_col = [x for x in ("counter_value", "value") if x in cols][0]
-        q = f"select {name_col}, {cn_col}, {val_col} from counters_collection"
-        for kname, cname, val in c.execute(q):
+        q = f"select {name_col}, {cn_col}, {val_col}, dispatch_id from counters_collection"
+        for kname, cname, val, did in c.execute(q):
             agg[short(kname)][cname] += val
+            disp[short(kname)].add(did)
+    if as_json:
+        import json
+        out = {k: dict(d, dispatches=len(disp[k])) for k, d in agg.items()}
+        with open(as_json, "w") as f:
+            json.dump(out, f, indent=1, sort_keys=True)
     for k, d in sorted(agg.items()):
-        print(k)
+        print(f"{k}  (dispatches: {len(disp[k])})")
         for cn, v in sorted(d.items()):
             print(f"   {cn:32s} {v:18.4g}")
 
@@ -56,5 +63,7 @@ def pmc(dbs):
 if __name__ == "__main__":
     if sys.argv[1] == "trace":
         trace(sys.argv[2])
+    elif sys.argv[1] == "pmcjson":
+        pmc(sys.argv[3:], as_json=sys.argv[2])
     else:
         pmc(sys.argv[2:])
