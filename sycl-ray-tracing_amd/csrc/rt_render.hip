@@ -138,6 +138,13 @@ struct LdsStack {
 #define RT_LDS_CAP_CLOSEST 16
 #define RT_LDS_CAP_ANY 16
 
+// Static wave-strided work assignment: wave w of the grid takes items
+// [w*64, w*64+64), then strides by the grid's wave count. (A shared atomic
+// ticket per 64 items serialized ~4k atomics on one address per launch:
+// ~45 us even for an empty queue.)
+__device__ __forceinline__ int wave_gid() { return (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6); }
+__device__ __forceinline__ int wave_count() { return (int)((gridDim.x * blockDim.x) >> 6); }
+
 // One ticket of 64 work items per wave.
 __device__ __forceinline__ int wave_ticket(int32_t* ticket)
 {
@@ -174,16 +181,14 @@ __global__ __launch_bounds__(256) void k_init(rtk::WaveView W, int32_t* act_coun
 }
 
 template <bool STATS>
-__global__ __launch_bounds__(256) void k_step(rtk::WaveView W, const int32_t* act_in_count, int32_t* act_out_count,
+__global__ __launch_bounds__(256, 3) void k_step(rtk::WaveView W, const int32_t* act_in_count, int32_t* act_out_count,
                                               unsigned long long* stats)
 {
     const int n = *act_in_count;
     rtk::Stats st;
     if (STATS)
         for (int i = 0; i < RT_STAT_COUNT; i++) st.c[i] = 0;
-    for (;;) {
-        const int base = wave_ticket(W.counters + C_TK_STEP);
-        if (base >= n) break;
+    for (int base = wave_gid() * 64; base < n; base += wave_count() * 64) {
         const int idx = base + lane_id();
         rtk::Emit e;
         e.mask = 0;
@@ -221,7 +226,7 @@ struct LdsIdx {
 };
 
 template <bool STATS>
-__global__ __launch_bounds__(256) void k_fast_closest(rtk::WaveView W, unsigned long long* stats)
+__global__ __launch_bounds__(256, 5) void k_fast_closest(rtk::WaveView W, unsigned long long* stats)
 {
     __shared__ uint32_t s_r[RT_LDS_CAP_FAST * 256];
     LdsIdx<RT_LDS_CAP_FAST> stk{s_r + threadIdx.x};
@@ -231,9 +236,7 @@ __global__ __launch_bounds__(256) void k_fast_closest(rtk::WaveView W, unsigned 
     rtk::Stats st;
     if (STATS)
         for (int i = 0; i < RT_STAT_COUNT; i++) st.c[i] = 0;
-    for (;;) {
-        const int base = wave_ticket(W.counters + C_TK_CLOSEST);
-        if (base >= total) break;
+    for (int base = wave_gid() * 64; base < total; base += wave_count() * 64) {
         const int idx = base + lane_id();
         bool fail = false;
         rtk::RayRec r;
@@ -257,7 +260,7 @@ __global__ __launch_bounds__(256) void k_fast_closest(rtk::WaveView W, unsigned 
 }
 
 template <bool STATS>
-__global__ __launch_bounds__(256) void k_fast_any(rtk::WaveView W, unsigned long long* stats)
+__global__ __launch_bounds__(256, 5) void k_fast_any(rtk::WaveView W, unsigned long long* stats)
 {
     __shared__ uint32_t s_r[RT_LDS_CAP_FAST * 256];
     LdsIdx<RT_LDS_CAP_FAST> stk{s_r + threadIdx.x};
@@ -265,9 +268,7 @@ __global__ __launch_bounds__(256) void k_fast_any(rtk::WaveView W, unsigned long
     rtk::Stats st;
     if (STATS)
         for (int i = 0; i < RT_STAT_COUNT; i++) st.c[i] = 0;
-    for (;;) {
-        const int base = wave_ticket(W.counters + C_TK_ANY);
-        if (base >= total) break;
+    for (int base = wave_gid() * 64; base < total; base += wave_count() * 64) {
         const int idx = base + lane_id();
         bool fail = false;
         rtk::RayRec r;
@@ -309,6 +310,7 @@ __global__ __launch_bounds__(256, 4) void k_exact_closest(rtk::WaveView W, unsig
     const int par = W.park_par;
     const int n_res = min(W.counters[C_PARKC0 + par], W.park_cap);
     const int total = n_res + W.counters[C_FBC];
+    if (total == 0) return;
     rtk::Stats st;
     if (STATS)
         for (int i = 0; i < RT_STAT_COUNT; i++) st.c[i] = 0;
@@ -373,6 +375,7 @@ __global__ __launch_bounds__(256, 4) void k_exact_any(rtk::WaveView W, unsigned 
     const int par = W.park_par;
     const int n_res = min(W.counters[C_PARKA0 + par], W.park_cap);
     const int total = n_res + W.counters[C_FBA];
+    if (total == 0) return;
     rtk::Stats st;
     if (STATS)
         for (int i = 0; i < RT_STAT_COUNT; i++) st.c[i] = 0;
@@ -583,7 +586,7 @@ static int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounce
     const int threads = 256;
     const int step_blocks = std::min((n + threads - 1) / threads, dev_cus * 8);
     const int trace_blocks = dev_cus * 4;  // exact kernels: persistent, 4 blocks of 256 per CU
-    const int fast_blocks = dev_cus * 4;   // fast kernels: persistent (LDS stack 32 KB per block)
+    const int fast_blocks = dev_cus * 8;   // fast kernels: wave-strided; 5 blocks (32 KB LDS each) resident per CU
     rtk::WaveView W{};
     W.park_cap = 1 << 16;
     W.spill_lanes = trace_blocks * threads;
