@@ -274,172 +274,6 @@ RT_HD int fast_query_any(const RtSceneView& S, V3 o, V3 d, STK& stk, Stats* st)
     }
 }
 
-// ----------------------------------------------------- resumable fast walks
-// fast_closest / fast_query_any cut into one-node steps, so a lane whose
-// query ends takes the next query at once (lane refill in the kernels).
-struct FastC {
-    V3 o, d;
-    RayB rb;
-    FastHit h;
-    int sp, cur;
-};
-
-RT_HD bool fastc_begin(FastC& F, V3 o, V3 d, Stats* st)
-{
-    F.o = o;
-    F.d = d;
-    F.h.t = __builtin_inff();
-    F.h.t2 = __builtin_inff();
-    F.h.k = -1;
-    F.h.tie = false;
-    F.h.ovf = false;
-    F.sp = 0;
-    F.cur = 0;
-    if (st) st->c[RT_STAT_RAYS]++;
-    if (rt_isnan(d.x) || rt_isnan(d.y) || rt_isnan(d.z) || rt_isnan(o.x) || rt_isnan(o.y) || rt_isnan(o.z)) {
-        F.h.t = -1.0f;
-        return false;
-    }
-    F.rb = rayb_setup(o, d);
-    return true;
-}
-
-// One BVH node; false when the walk is over (h final, or h.ovf).
-template <class STK>
-RT_HD bool fastc_step(const RtSceneView& S, FastC& F, STK& stk, Stats* st)
-{
-    const BvhNodeR n = load_bvh(S.bvh, F.cur);
-    if (st) st->c[RT_STAT_VOL] += 2;
-    const float tmax = F.h.t + F.h.t * RT_T2_WINDOW;
-    float tl, tr;
-    const bool hl = n.lcount >= 0 && box_hit(n.lmin, n.lmax, F.rb, tmax, tl);
-    const bool hr = n.rcount >= 0 && box_hit(n.rmin, n.rmax, F.rb, tmax, tr);
-    if (hl && n.lcount > 0) fast_leaf(S, n.left, n.lcount, F.o, F.d, F.h, st);
-    if (hr && n.rcount > 0) fast_leaf(S, n.right, n.rcount, F.o, F.d, F.h, st);
-    const bool il = hl && n.lcount == 0, ir = hr && n.rcount == 0;
-    int next = -1;
-    if (il && ir) {
-        const bool lfirst = tl <= tr;
-        next = lfirst ? n.left : n.right;
-        if (F.sp == STK::CAP) {
-            F.h.ovf = true;
-            return false;
-        }
-        stk.set_rec(F.sp++, (uint32_t)(lfirst ? n.right : n.left));
-    } else if (il) {
-        next = n.left;
-    } else if (ir) {
-        next = n.right;
-    }
-    if (next >= 0) {
-        F.cur = next;
-        return true;
-    }
-    if (F.sp == 0) {
-        if (F.h.k < 0) F.h.t = -1.0f;
-        return false;
-    }
-    F.cur = (int)stk.rec(--F.sp);
-    return true;
-}
-
-// Verification of a finished closest walk (see fast_query_closest): true =
-// (t_out, k_out) is the reference's answer; false = use the exact walk.
-RT_HD bool fastc_verify(const RtSceneView& S, const FastC& F, float& t_out, int& k_out, Stats* st)
-{
-    if (F.h.ovf) return false;
-    if (F.h.k < 0) {
-        t_out = -1.0f;
-        k_out = -1;
-        return true;
-    }
-    if (F.h.tie) return false;
-    RayK K;
-    ray_setup(F.o, F.d, K);
-    const float t2 = __builtin_fminf(F.h.t2, F.h.t + F.h.t * RT_T2_WINDOW);
-    if (!chain_ok(S, K, S.leaf_of[F.h.k], true, t2, st)) return false;
-    t_out = F.h.t;
-    k_out = F.h.k;
-    return true;
-}
-
-struct FastA {
-    V3 o, d;
-    RayB rb;
-    int sp, cur;
-    int result;  // -2 running, 0 / 1 answer, -1 overflow
-};
-
-RT_HD bool fasta_begin(FastA& F, V3 o, V3 d, Stats* st)
-{
-    F.o = o;
-    F.d = d;
-    F.sp = 0;
-    F.cur = 0;
-    F.result = -2;
-    if (st) st->c[RT_STAT_ANY_RAYS]++;
-    if (rt_isnan(d.x) || rt_isnan(d.y) || rt_isnan(d.z) || rt_isnan(o.x) || rt_isnan(o.y) || rt_isnan(o.z)) {
-        F.result = 0;
-        return false;
-    }
-    F.rb = rayb_setup(o, d);
-    return true;
-}
-
-template <class STK>
-RT_HD bool fasta_step(const RtSceneView& S, FastA& F, STK& stk, Stats* st)
-{
-    const BvhNodeR n = load_bvh(S.bvh, F.cur);
-    if (st) st->c[RT_STAT_ANY_VOL] += 2;
-    float tl, tr;
-    const bool hl = n.lcount >= 0 && box_hit(n.lmin, n.lmax, F.rb, __builtin_inff(), tl);
-    const bool hr = n.rcount >= 0 && box_hit(n.rmin, n.rmax, F.rb, __builtin_inff(), tr);
-    for (int side = 0; side < 2; side++) {
-        const bool hit = side ? hr : hl;
-        const int cnt = side ? n.rcount : n.lcount;
-        if (!hit || cnt <= 0) continue;
-        const int first = side ? n.right : n.left;
-        if (st) st->c[RT_STAT_ANY_TRI] += cnt;
-        for (int j = 0; j < cnt; j++) {
-            float t;
-            if (tri_test(S.bvh_tri4, first + j, F.o, F.d, t)) {
-                RayK K;
-                ray_setup(F.o, F.d, K);
-                const int k = (int)rt_asuint(S.bvh_tri4[3 * (first + j)].w);
-                if (chain_ok(S, K, S.leaf_of[k], false, 0.0f, st)) {
-                    F.result = 1;
-                    return false;
-                }
-            }
-        }
-    }
-    const bool il = hl && n.lcount == 0, ir = hr && n.rcount == 0;
-    int next = -1;
-    if (il && ir) {
-        const bool lfirst = tl <= tr;
-        next = lfirst ? n.left : n.right;
-        if (F.sp == STK::CAP) {
-            F.result = -1;
-            return false;
-        }
-        stk.set_rec(F.sp++, (uint32_t)(lfirst ? n.right : n.left));
-    } else if (il) {
-        next = n.left;
-    } else if (ir) {
-        next = n.right;
-    }
-    if (next >= 0) {
-        F.cur = next;
-        return true;
-    }
-    if (F.sp == 0) {
-        F.result = 0;
-        return false;
-    }
-    F.cur = (int)stk.rec(--F.sp);
-    return true;
-}
-
 // Plain-array node-index stack (host build).
 template <int N>
 struct IdxStack {

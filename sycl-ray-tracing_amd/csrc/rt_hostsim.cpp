@@ -102,16 +102,9 @@ static int run_wave_host(rt_context* c, int w, int h, int spp, int bounces, cons
             for (int idx = 0; idx < nq; idx++) {
                 uint32_t target;
                 rtk::RayRec r = rtk::queue_item(W, counters, rtk::RK_CONT, last_kind, idx, target);
-                float t = -1.0f;
-                int k = -1;
-                rtk::FastC F;  // the device kernels' step form, run to completion
-                bool ok = true;
-                if (rtk::fastc_begin(F, rtk::v3of(r.o), rtk::v3of(r.d), ps)) {
-                    while (rtk::fastc_step(W.S, F, fst, ps)) {
-                    }
-                    ok = rtk::fastc_verify(W.S, F, t, k, ps);
-                }
-                if (ok) {
+                float t;
+                int k;
+                if (rtk::fast_query_closest(W.S, rtk::v3of(r.o), rtk::v3of(r.d), fst, t, k, ps)) {
                     rtk::finish_closest(W, target, rtk::v3of(r.o), rtk::v3of(r.d), t, k);
                 } else {
                     r.d.w = rt_asfloat(target & 7u);
@@ -122,11 +115,7 @@ static int run_wave_host(rt_context* c, int w, int h, int spp, int bounces, cons
             for (int idx = 0; idx < nqa; idx++) {
                 uint32_t target;
                 rtk::RayRec r = rtk::queue_item(W, counters, rtk::RK_ESH, rtk::RK_BENV, idx, target);
-                rtk::FastA F;
-                if (rtk::fasta_begin(F, rtk::v3of(r.o), rtk::v3of(r.d), ps))
-                    while (rtk::fasta_step(W.S, F, fst, ps)) {
-                    }
-                const int a = F.result;
+                const int a = rtk::fast_query_any(W.S, rtk::v3of(r.o), rtk::v3of(r.d), fst, ps);
                 if (a >= 0) {
                     rtk::finish_any(W, target, a == 1);
                 } else {

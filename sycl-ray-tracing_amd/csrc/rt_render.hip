@@ -216,7 +216,6 @@ __global__ __launch_bounds__(256, 3) void k_step(rtk::WaveView W, const int32_t*
 // whose stack would overflow) goes to the fallback list for
 // k_exact_closest / k_exact_any.
 #define RT_LDS_CAP_FAST 32
-#define RT_REFILL 16  // refill a wave's idle lanes once this many are idle
 
 template <int N>
 struct LdsIdx {
@@ -226,23 +225,6 @@ struct LdsIdx {
     __device__ __forceinline__ void set_rec(int i, uint32_t v) { r[i * 256] = v; }
 };
 
-// Work split for the lane-refill kernels: wave w owns items [lo, hi) of
-// the kernel's work list (at least 256 per wave so small iterations use few
-// waves); its lanes refill from that pool, no atomics.
-struct WavePool {
-    int lo, hi;
-};
-__device__ __forceinline__ WavePool wave_pool(int total)
-{
-    const int nw = wave_count();
-    const int chunk = max(256, (total + nw - 1) / nw);
-    const long lo = (long)wave_gid() * chunk;
-    WavePool p;
-    p.lo = (int)min((long)total, lo);
-    p.hi = (int)min((long)total, lo + chunk);
-    return p;
-}
-
 template <bool STATS>
 __global__ __launch_bounds__(256, 5) void k_fast_closest(rtk::WaveView W, unsigned long long* stats)
 {
@@ -251,44 +233,27 @@ __global__ __launch_bounds__(256, 5) void k_fast_closest(rtk::WaveView W, unsign
     const int last_kind = W.any_rays ? rtk::RK_BL : rtk::RK_BENV;
     int total = 0;
     for (int k = rtk::RK_CONT; k <= last_kind; k++) total += W.counters[C_Q0 + k];
-    const WavePool pool = wave_pool(total);
-    if (pool.lo >= pool.hi) return;
     rtk::Stats st;
     if (STATS)
         for (int i = 0; i < RT_STAT_COUNT; i++) st.c[i] = 0;
-    rtk::FastC F;
-    bool has = false;
-    uint32_t target = 0;
-    int next = pool.lo;
-    for (;;) {
-        const bool need = !has;
-        const unsigned long long bneed = __ballot(need);
-        const int nneed = __popcll(bneed);
-        if (next < pool.hi && (nneed >= RT_REFILL || nneed == 64)) {
-            if (need) {
-                const int idx = next + __popcll(bneed & ((1ull << lane_id()) - 1ull));
-                if (idx < pool.hi) {
-                    const rtk::RayRec r = rtk::queue_item(W, W.counters + C_Q0, rtk::RK_CONT, last_kind, idx, target);
-                    has = rtk::fastc_begin(F, rtk::v3of(r.o), rtk::v3of(r.d), STATS ? &st : nullptr);
-                    if (!has) rtk::finish_closest(W, target, F.o, F.d, -1.0f, -1);
-                }
-            }
-            next += nneed;
-        }
-        if (!__any(has)) {
-            if (next >= pool.hi) break;
-            continue;
-        }
-        if (has && !rtk::fastc_step(W.S, F, stk, STATS ? &st : nullptr)) {
+    for (int base = wave_gid() * 64; base < total; base += wave_count() * 64) {
+        const int idx = base + lane_id();
+        bool fail = false;
+        rtk::RayRec r;
+        uint32_t target = 0;
+        if (idx < total) {
+            r = rtk::queue_item(W, W.counters + C_Q0, rtk::RK_CONT, last_kind, idx, target);
             float t;
             int k;
-            if (rtk::fastc_verify(W.S, F, t, k, STATS ? &st : nullptr)) {
-                rtk::finish_closest(W, target, F.o, F.d, t, k);
-            } else {
-                const int f = atomicAdd(W.counters + C_FBC, 1);
-                W.fb_c[f] = rtk::RayRec{rtk::f4(F.o, rt_asfloat(target >> 3)), rtk::f4(F.d, rt_asfloat(target & 7u))};
-            }
-            has = false;
+            if (rtk::fast_query_closest(W.S, rtk::v3of(r.o), rtk::v3of(r.d), stk, t, k, STATS ? &st : nullptr))
+                rtk::finish_closest(W, target, rtk::v3of(r.o), rtk::v3of(r.d), t, k);
+            else
+                fail = true;
+        }
+        const int f = wave_append(W.counters + C_FBC, fail);
+        if (fail) {
+            r.d.w = rt_asfloat(target & 7u);
+            W.fb_c[f] = r;
         }
     }
     flush_stats<STATS>(st, stats);
@@ -300,42 +265,26 @@ __global__ __launch_bounds__(256, 5) void k_fast_any(rtk::WaveView W, unsigned l
     __shared__ uint32_t s_r[RT_LDS_CAP_FAST * 256];
     LdsIdx<RT_LDS_CAP_FAST> stk{s_r + threadIdx.x};
     const int total = W.counters[C_Q0 + rtk::RK_ESH] + W.counters[C_Q0 + rtk::RK_BENV];
-    const WavePool pool = wave_pool(total);
-    if (pool.lo >= pool.hi) return;
     rtk::Stats st;
     if (STATS)
         for (int i = 0; i < RT_STAT_COUNT; i++) st.c[i] = 0;
-    rtk::FastA F;
-    bool has = false;
-    uint32_t target = 0;
-    int next = pool.lo;
-    for (;;) {
-        const bool need = !has;
-        const unsigned long long bneed = __ballot(need);
-        const int nneed = __popcll(bneed);
-        if (next < pool.hi && (nneed >= RT_REFILL || nneed == 64)) {
-            if (need) {
-                const int idx = next + __popcll(bneed & ((1ull << lane_id()) - 1ull));
-                if (idx < pool.hi) {
-                    const rtk::RayRec r = rtk::queue_item(W, W.counters + C_Q0, rtk::RK_ESH, rtk::RK_BENV, idx, target);
-                    has = rtk::fasta_begin(F, rtk::v3of(r.o), rtk::v3of(r.d), STATS ? &st : nullptr);
-                    if (!has) rtk::finish_any(W, target, false);
-                }
-            }
-            next += nneed;
+    for (int base = wave_gid() * 64; base < total; base += wave_count() * 64) {
+        const int idx = base + lane_id();
+        bool fail = false;
+        rtk::RayRec r;
+        uint32_t target = 0;
+        if (idx < total) {
+            r = rtk::queue_item(W, W.counters + C_Q0, rtk::RK_ESH, rtk::RK_BENV, idx, target);
+            const int a = rtk::fast_query_any(W.S, rtk::v3of(r.o), rtk::v3of(r.d), stk, STATS ? &st : nullptr);
+            if (a >= 0)
+                rtk::finish_any(W, target, a == 1);
+            else
+                fail = true;
         }
-        if (!__any(has)) {
-            if (next >= pool.hi) break;
-            continue;
-        }
-        if (has && !rtk::fasta_step(W.S, F, stk, STATS ? &st : nullptr)) {
-            if (F.result >= 0) {
-                rtk::finish_any(W, target, F.result == 1);
-            } else {
-                const int f = atomicAdd(W.counters + C_FBA, 1);
-                W.fb_a[f] = rtk::RayRec{rtk::f4(F.o, rt_asfloat(target >> 3)), rtk::f4(F.d, rt_asfloat(target & 7u))};
-            }
-            has = false;
+        const int f = wave_append(W.counters + C_FBA, fail);
+        if (fail) {
+            r.d.w = rt_asfloat(target & 7u);
+            W.fb_a[f] = r;
         }
     }
     flush_stats<STATS>(st, stats);
@@ -347,6 +296,7 @@ __global__ __launch_bounds__(256, 5) void k_fast_any(rtk::WaveView W, unsigned l
 // queries of the last launch first, then the queues) once REFILL lanes are
 // idle; a query that has taken W.budget steps parks at its next node
 // boundary. Work list order: parked, then the ray kinds in queue order.
+#define RT_REFILL 16
 
 template <bool STATS>
 __global__ __launch_bounds__(256, 4) void k_exact_closest(rtk::WaveView W, unsigned long long* stats)
