@@ -62,7 +62,7 @@ struct RtSceneView {
     int32_t n_tris, chain_monotone, pad1, pad2;  // chain_monotone: see rt_fast.h chain_ok
     // search BVH + octree back-links for the verification walk
     const BvhNode* bvh;        // [0] = root (its two boxes are the scene's halves)
-    const float4_* bvh_tri4;   // 3 records per triangle in BVH leaf order: {a.xyz, k}, {e1}, {e2}
+    const float4_* bvh_tri4;   // 3 records per triangle in BVH leaf order: {a.xyz, k}, {e1, leaf record}, {e2}
     const int32_t* parent;     // octree record -> parent record (-1 for the root)
     const int32_t* leaf_of;    // leaf-order triangle k -> its octree leaf record
 };

@@ -86,6 +86,7 @@ RT_HD BvhNodeR load_bvh(const BvhNode* nodes, int i)
 struct FastHit {
     float t, t2;  // closest M-T hit (-1: none), smallest other hit seen (window-bounded)
     int k;        // leaf-order triangle of t
+    int leaf;     // its octree leaf record
     bool tie;     // another triangle hit at exactly t
     bool ovf;     // the bounded stack overflowed: answer unknown
 };
@@ -100,6 +101,7 @@ RT_HD void fast_leaf(const RtSceneView& S, int first, int count, V3 o, V3 d, Fas
                 h.t2 = h.t;
                 h.t = t;
                 h.k = (int)rt_asuint(S.bvh_tri4[3 * i].w);
+                h.leaf = (int)rt_asuint(S.bvh_tri4[3 * i + 1].w);
                 h.tie = false;
             } else if (t == h.t) {
                 h.tie = true;
@@ -211,7 +213,7 @@ RT_HD bool fast_query_closest(const RtSceneView& S, V3 o, V3 d, STK& stk, float&
     RayK K;
     ray_setup(o, d, K);
     const float t2 = __builtin_fminf(h.t2, h.t + h.t * RT_T2_WINDOW);
-    if (!chain_ok(S, K, S.leaf_of[h.k], true, t2, st)) return false;
+    if (!chain_ok(S, K, h.leaf, true, t2, st)) return false;
     t_out = h.t;
     k_out = h.k;
     return true;
@@ -248,8 +250,7 @@ RT_HD int fast_query_any(const RtSceneView& S, V3 o, V3 d, STK& stk, Stats* st)
                         ray_setup(o, d, K);
                         kset = true;
                     }
-                    const int k = (int)rt_asuint(S.bvh_tri4[3 * (first + j)].w);
-                    if (chain_ok(S, K, S.leaf_of[k], false, 0.0f, st)) return 1;
+                    if (chain_ok(S, K, (int)rt_asuint(S.bvh_tri4[3 * (first + j) + 1].w), false, 0.0f, st)) return 1;
                 }
             }
         }

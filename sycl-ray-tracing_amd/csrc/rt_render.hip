@@ -215,7 +215,7 @@ __global__ __launch_bounds__(256, 3) void k_step(rtk::WaveView W, const int32_t*
 // node indices in LDS; a query whose answer needs the exact octree walk (or
 // whose stack would overflow) goes to the fallback list for
 // k_exact_closest / k_exact_any.
-#define RT_LDS_CAP_FAST 32
+#define RT_LDS_CAP_FAST 24
 
 template <int N>
 struct LdsIdx {
@@ -226,7 +226,7 @@ struct LdsIdx {
 };
 
 template <bool STATS>
-__global__ __launch_bounds__(256, 5) void k_fast_closest(rtk::WaveView W, unsigned long long* stats)
+__global__ __launch_bounds__(256, 6) void k_fast_closest(rtk::WaveView W, unsigned long long* stats)
 {
     __shared__ uint32_t s_r[RT_LDS_CAP_FAST * 256];
     LdsIdx<RT_LDS_CAP_FAST> stk{s_r + threadIdx.x};
@@ -260,7 +260,7 @@ __global__ __launch_bounds__(256, 5) void k_fast_closest(rtk::WaveView W, unsign
 }
 
 template <bool STATS>
-__global__ __launch_bounds__(256, 5) void k_fast_any(rtk::WaveView W, unsigned long long* stats)
+__global__ __launch_bounds__(256, 6) void k_fast_any(rtk::WaveView W, unsigned long long* stats)
 {
     __shared__ uint32_t s_r[RT_LDS_CAP_FAST * 256];
     LdsIdx<RT_LDS_CAP_FAST> stk{s_r + threadIdx.x};

@@ -678,6 +678,7 @@ void build_search_bvh(FlatBvh& out)
         out.bvh_tri4[3 * (size_t)i] = out.tri4[3 * (size_t)k];
         std::memcpy(&out.bvh_tri4[3 * (size_t)i].w, &k, 4);
         out.bvh_tri4[3 * (size_t)i + 1] = out.tri4[3 * (size_t)k + 1];
+        std::memcpy(&out.bvh_tri4[3 * (size_t)i + 1].w, &out.leaf_of[k], 4);  // octree leaf record
         out.bvh_tri4[3 * (size_t)i + 2] = out.tri4[3 * (size_t)k + 2];
     }
     if (out.bvh.empty()) {  // no triangles: a root with two empty slots
