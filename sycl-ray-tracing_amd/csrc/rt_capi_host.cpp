@@ -1,6 +1,7 @@
 // rt_capi_host.cpp — the backend-independent half of the C ABI
 // (include/rt_hip.h): argument checking, host scene preparation, host
 // helpers. The compute half lives in rt_render.hip (gfx950).
+#include <algorithm>
 #include <cstring>
 #include <mutex>
 
@@ -36,6 +37,9 @@ RtSceneView rt_host_view(const rt_context* c)
     v.env = c->env.data();
     v.env_lum = c->env_lum.data();
     v.cdf = c->cdf.data();
+    v.cdf_row = c->cdf_row.data();
+    v.cdf_coarse = c->cdf_coarse.data();
+    v.cdf_cw = c->cdf_cw;
     v.n_emissive = (int)c->emissive.size();
     v.n_spheres = (int)(c->spheres.size() / 2);
     v.ew = c->ew;
@@ -203,6 +207,12 @@ int rt_set_env(rt_context* c, const float* px, int w, int h, int ch, const float
     c->cdf.resize(n);
     rt::env_luminance_cdf(px, w, h, ch, c->env_lum.data(), c->cdf.data());
     if (cdf) c->cdf.assign(cdf, cdf + n);
+    c->cdf_row.resize(h);
+    for (int y = 0; y < h; y++) c->cdf_row[y] = c->cdf[(size_t)y * w + w - 1];
+    c->cdf_cw = w / 32;
+    c->cdf_coarse.resize(std::max<size_t>(1, (size_t)h * c->cdf_cw));
+    for (int y = 0; y < h; y++)
+        for (int j = 0; j < c->cdf_cw; j++) c->cdf_coarse[(size_t)y * c->cdf_cw + j] = c->cdf[(size_t)y * w + 32 * j + 31];
     c->have_env = true;
     c->dirty = true;
     return RT_OK;

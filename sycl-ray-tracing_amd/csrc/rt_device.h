@@ -58,8 +58,10 @@ struct RtSceneView {
     const float4_* env;
     const float* env_lum;
     const float* cdf;
+    const float* cdf_row;     // [eh]  cdf of each row's last texel
+    const float* cdf_coarse;  // [eh][cdf_cw]  cdf[y*ew + 32j + 31]
     int32_t n_emissive, n_spheres, ew, eh;
-    int32_t n_tris, chain_monotone, pad1, pad2;  // chain_monotone: see rt_fast.h chain_ok
+    int32_t n_tris, chain_monotone, cdf_cw, pad2;  // chain_monotone: see rt_fast.h chain_ok
     // search BVH + octree back-links for the verification walk
     const BvhNode* bvh;        // [0] = root (its two boxes are the scene's halves)
     const float4_* bvh_tri4;   // 3 records per triangle in BVH leaf order: {a.xyz, k}, {e1, leaf record}, {e2}

@@ -60,7 +60,7 @@ enum {
 
 struct Backend {
     DevBuf nodes, tri4, prim2k, mat_idx, mats, emissive, spheres, env, env_lum, cdf;
-    DevBuf bvh, bvh_tri4, parent, leaf_of;
+    DevBuf bvh, bvh_tri4, parent, leaf_of, cdf_row, cdf_coarse;
     DevBuf stats;     // RT_STAT_COUNT u64
     DevBuf wave;      // path state, pending records, results, queues, lists
     DevBuf counters;  // C_COUNT int32
@@ -520,7 +520,8 @@ void rt_backend_destroy(rt_context* c)
     if (!b) return;
     (void)hipSetDevice(c->device);
     DevBuf* all[] = {&b->nodes, &b->tri4, &b->prim2k, &b->mat_idx, &b->mats, &b->emissive, &b->spheres, &b->env,
-                     &b->env_lum, &b->cdf, &b->bvh, &b->bvh_tri4, &b->parent, &b->leaf_of, &b->stats, &b->wave,
+                     &b->env_lum, &b->cdf, &b->bvh, &b->bvh_tri4, &b->parent, &b->leaf_of, &b->cdf_row, &b->cdf_coarse,
+                     &b->stats, &b->wave,
                      &b->counters, &b->xy, &b->fb};
     for (DevBuf* d : all)
         if (d->p) (void)hipFree(d->p);
@@ -546,6 +547,7 @@ int rt_backend_upload(rt_context* c)
         (r = upload(c, b->env_lum, c->env_lum)) || (r = upload(c, b->cdf, c->cdf)) ||
         (r = upload(c, b->bvh, c->flat.bvh)) || (r = upload(c, b->bvh_tri4, c->flat.bvh_tri4)) ||
         (r = upload(c, b->parent, c->flat.parent)) || (r = upload(c, b->leaf_of, c->flat.leaf_of)) ||
+        (r = upload(c, b->cdf_row, c->cdf_row)) || (r = upload(c, b->cdf_coarse, c->cdf_coarse)) ||
         (r = ensure(c, b->stats, RT_STAT_COUNT * sizeof(unsigned long long))) ||
         (r = ensure(c, b->counters, C_COUNT * sizeof(int32_t))))
         return r;
@@ -560,6 +562,9 @@ int rt_backend_upload(rt_context* c)
     v.env = (const float4_*)b->env.p;
     v.env_lum = (const float*)b->env_lum.p;
     v.cdf = (const float*)b->cdf.p;
+    v.cdf_row = (const float*)b->cdf_row.p;
+    v.cdf_coarse = (const float*)b->cdf_coarse.p;
+    v.cdf_cw = c->cdf_cw;
     v.n_emissive = (int)c->emissive.size();
     v.n_spheres = (int)(c->spheres.size() / 2);
     v.ew = c->ew;

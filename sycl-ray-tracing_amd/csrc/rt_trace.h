@@ -790,10 +790,16 @@ RT_HD void cdf_search(const RtSceneView& S, float value, int& x, int& y, Stats* 
     int lower = 0, upper = S.eh - 1;
     const int xi = S.ew - 1;
     int probes = 0;
+    (void)xi;
+    // Same probes and comparisons as the reference; the values come from
+    // exact copies laid out for locality: cdf_row[y] = cdf[y*ew + ew-1]
+    // (the row search reads one 4-KB array) and cdf_coarse[y][j] =
+    // cdf[y*ew + 32j + 31] (for a power-of-two width the first column probes
+    // all land there, the rest inside one 128-B line).
     while (lower < upper) {
         int yi = (lower + upper) / 2;
         probes++;
-        if (value < S.cdf[yi * S.ew + xi])
+        if (value < S.cdf_row[yi])
             upper = yi;
         else
             lower = yi + 1;
@@ -801,10 +807,13 @@ RT_HD void cdf_search(const RtSceneView& S, float value, int& x, int& y, Stats* 
     y = rt_maxi(rt_mini(lower, S.eh), 0);
     lower = 0;
     upper = S.ew - 1;
+    const float* row = S.cdf + (size_t)y * S.ew;
+    const float* crow = S.cdf_coarse + (size_t)y * S.cdf_cw;
     while (lower < upper) {
         int xm = (lower + upper) / 2;
         probes++;
-        if (value < S.cdf[y * S.ew + xm])
+        const float c = ((xm & 31) == 31 && (xm >> 5) < S.cdf_cw) ? crow[xm >> 5] : row[xm];
+        if (value < c)
             upper = xm;
         else
             lower = xm + 1;
