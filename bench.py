@@ -58,11 +58,14 @@ BYTES = {"box": 32, "tri": 48, "verify": 64, "ray": 40, "mat": 32, "env": 16, "c
 
 
 def algo_bytes(st: dict, kernel: str) -> float:
-    if kernel == "trace_closest":
-        return (BYTES["box"] * st["vol"] + BYTES["tri"] * st["tri"] + BYTES["verify"] * st["verify"] +
-                BYTES["ray"] * st["rays"])
-    if kernel == "trace_any":
-        return BYTES["box"] * st["any_vol"] + BYTES["tri"] * st["any_tri"] + BYTES["ray"] * st["any_rays"]
+    # k_trace answers every closest-hit and occlusion query; its exact-walk
+    # role (st["fallback"] queries, ~1e-6 of them) shares the box / triangle
+    # counters, so those bytes are booked here too (an overcount of < 0.1%).
+    if kernel == "trace":
+        return (BYTES["box"] * (st["vol"] + st["any_vol"]) + BYTES["tri"] * (st["tri"] + st["any_tri"]) +
+                BYTES["verify"] * st["verify"] + BYTES["ray"] * (st["rays"] + st["any_rays"]))
+    if kernel == "other":
+        return 0.0
     return BYTES["mat"] * st["mat"] + BYTES["env"] * st["env"] + BYTES["cdf"] * st["cdf"]
 
 
@@ -194,7 +197,7 @@ def main():
 
     roofline = None
     if stats is not None:
-        dom = max(("trace_closest", "trace_any", "step"), key=lambda k: ktime[k][0])
+        dom = max(("trace", "step"), key=lambda k: ktime[k][0])
         tot_ms, launches = ktime[dom]
         per_render = algo_bytes(stats, dom)          # the counter pass rendered one frame
         algo = per_render / max(launches / args.steps, 1)  # per launch

@@ -86,14 +86,95 @@ static int run_wave_host(rt_context* c, int w, int h, int spp, int bounces, cons
     }
     using FAST = rtk::ArrayStack<RT_HOSTSIM_SHORT_CAP>;
     const int last_kind = W.any_rays ? rtk::RK_BL : rtk::RK_BENV;
+    int32_t fbc[2] = {0, 0}, fba[2] = {0, 0};
     for (long it = 0;; it++) {
         const int par = (int)(it & 1);
-        W.park_par = par;
-        // fast queries through the search BVH; failures go to the fallback lists
+        // k_trace, exact roles: the walks the last iteration left (parked
+        // ones, then its fallback lists); each holds one r_park count of its slot
+        const int nrc = std::min(parkc[par], W.park_cap), nra = std::min(parka[par], W.park_cap);
+        const int nc = nrc + fbc[par], na = nra + fba[par];
+#pragma omp parallel
+        {
+            std::vector<uint32_t> spr(RT_STACK_CAP);
+            std::vector<float> spk(RT_STACK_CAP);
+            rtk::SpillStack<FAST> stk{FAST{}, spr.data(), spk.data()};
+            rtk::Stats* ps = c->stats_enabled ? &st[omp_get_thread_num()] : nullptr;
+#pragma omp for schedule(dynamic, 16)
+            for (int idx = 0; idx < nc; idx++) {
+                rtk::TravC T;
+                uint32_t target;
+                bool has;
+                if (idx < nrc) {
+                    target = rtk::travc_resume(&W.park_c[par][idx], T, stk);
+                    has = true;
+                } else {
+                    const rtk::RayRec r = W.fb_c[par][idx - nrc];
+                    target = (rt_asuint(r.o.w) << 3) | rt_asuint(r.d.w);
+                    if (ps) ps->c[RT_STAT_FALLBACK]++;
+                    has = rtk::travc_begin(W.S, T, rtk::v3of(r.o), rtk::v3of(r.d), ps);
+                    if (!has) {
+                        rtk::finish_closest(W, target, T.o, T.d, T.best_t, T.best_k);
+                        __atomic_fetch_sub(&W.r_park[target >> 3], 1, __ATOMIC_RELAXED);
+                    }
+                }
+                while (has) {
+                    if (!rtk::travc_step(W.S, T, stk, ps)) {
+                        rtk::finish_closest(W, target, T.o, T.d, T.best_t, T.best_k);
+                        __atomic_fetch_sub(&W.r_park[target >> 3], 1, __ATOMIC_RELAXED);
+                        break;
+                    }
+                    if (T.steps >= W.budget && rtk::travc_parkable(T)) {
+                        const int slot = __atomic_fetch_add(&parkc[par ^ 1], 1, __ATOMIC_RELAXED);
+                        if (slot < W.park_cap) {
+                            rtk::travc_park(T, stk, target, &W.park_c[par ^ 1][slot]);
+                            break;
+                        }
+                        T.steps = 0;
+                    }
+                }
+            }
+#pragma omp for schedule(dynamic, 16)
+            for (int idx = 0; idx < na; idx++) {
+                rtk::TravA T;
+                uint32_t target;
+                bool has;
+                if (idx < nra) {
+                    target = rtk::trava_resume(&W.park_a[par][idx], T, stk);
+                    has = true;
+                } else {
+                    const rtk::RayRec r = W.fb_a[par][idx - nra];
+                    target = (rt_asuint(r.o.w) << 3) | rt_asuint(r.d.w);
+                    if (ps) ps->c[RT_STAT_FALLBACK]++;
+                    has = rtk::trava_begin(W.S, T, rtk::v3of(r.o), rtk::v3of(r.d), ps);
+                    if (!has) {
+                        rtk::finish_any(W, target, false);
+                        __atomic_fetch_sub(&W.r_park[target >> 3], 1, __ATOMIC_RELAXED);
+                    }
+                }
+                while (has) {
+                    if (!rtk::trava_step(W.S, T, stk, ps)) {
+                        rtk::finish_any(W, target, T.hit);
+                        __atomic_fetch_sub(&W.r_park[target >> 3], 1, __ATOMIC_RELAXED);
+                        break;
+                    }
+                    if (T.steps >= W.budget && rtk::trava_parkable(T)) {
+                        const int slot = __atomic_fetch_add(&parka[par ^ 1], 1, __ATOMIC_RELAXED);
+                        if (slot < W.park_cap) {
+                            rtk::trava_park(T, stk, target, &W.park_a[par ^ 1][slot]);
+                            break;
+                        }
+                        T.steps = 0;
+                    }
+                }
+            }
+        }
+        // k_trace, fast roles: this iteration's queries through the search
+        // BVH; failures go to the fallback lists of the next iteration
         int nq = 0;
         for (int k = rtk::RK_CONT; k <= last_kind; k++) nq += counters[k];
         const int nqa = W.any_rays ? counters[rtk::RK_ESH] + counters[rtk::RK_BENV] : 0;
-        int fbc = 0, fba = 0;
+        int32_t* fbc_out = &fbc[par ^ 1];
+        int32_t* fba_out = &fba[par ^ 1];
 #pragma omp parallel
         {
             rtk::IdxStack<RT_HOSTSIM_FAST_CAP> fst;
@@ -108,7 +189,8 @@ static int run_wave_host(rt_context* c, int w, int h, int spp, int bounces, cons
                     rtk::finish_closest(W, target, rtk::v3of(r.o), rtk::v3of(r.d), t, k);
                 } else {
                     r.d.w = rt_asfloat(target & 7u);
-                    W.fb_c[__atomic_fetch_add(&fbc, 1, __ATOMIC_RELAXED)] = r;
+                    W.fb_c[par ^ 1][__atomic_fetch_add(fbc_out, 1, __ATOMIC_RELAXED)] = r;
+                    __atomic_fetch_add(&W.r_park[target >> 3], 1, __ATOMIC_RELAXED);
                 }
             }
 #pragma omp for schedule(dynamic, 64)
@@ -120,86 +202,15 @@ static int run_wave_host(rt_context* c, int w, int h, int spp, int bounces, cons
                     rtk::finish_any(W, target, a == 1);
                 } else {
                     r.d.w = rt_asfloat(target & 7u);
-                    W.fb_a[__atomic_fetch_add(&fba, 1, __ATOMIC_RELAXED)] = r;
+                    W.fb_a[par ^ 1][__atomic_fetch_add(fba_out, 1, __ATOMIC_RELAXED)] = r;
+                    __atomic_fetch_add(&W.r_park[target >> 3], 1, __ATOMIC_RELAXED);
                 }
             }
         }
-        // exact walks: parked queries, then the fallback lists
-        const int nrc = std::min(parkc[par], W.park_cap), nra = std::min(parka[par], W.park_cap);
-        const int nc = nrc + fbc, na = nra + fba;
-#pragma omp parallel
-        {
-            std::vector<uint32_t> spr(RT_STACK_CAP);
-            std::vector<float> spk(RT_STACK_CAP);
-            rtk::SpillStack<FAST> stk{FAST{}, spr.data(), spk.data()};
-            rtk::Stats* ps = c->stats_enabled ? &st[omp_get_thread_num()] : nullptr;
-#pragma omp for schedule(dynamic, 16)
-            for (int idx = 0; idx < nc; idx++) {
-                rtk::TravC T;
-                uint32_t target;
-                bool resumed = idx < nrc, has;
-                if (resumed) {
-                    target = rtk::travc_resume(&W.park_c[par][idx], T, stk);
-                    has = true;
-                } else {
-                    const rtk::RayRec r = W.fb_c[idx - nrc];
-                    target = (rt_asuint(r.o.w) << 3) | rt_asuint(r.d.w);
-                    if (ps) ps->c[RT_STAT_FALLBACK]++;
-                    has = rtk::travc_begin(W.S, T, rtk::v3of(r.o), rtk::v3of(r.d), ps);
-                    if (!has) rtk::finish_closest(W, target, T.o, T.d, T.best_t, T.best_k);
-                }
-                while (has) {
-                    if (!rtk::travc_step(W.S, T, stk, ps)) {
-                        rtk::finish_closest(W, target, T.o, T.d, T.best_t, T.best_k);
-                        if (resumed) __atomic_fetch_sub(&W.r_park[target >> 3], 1, __ATOMIC_RELAXED);
-                        break;
-                    }
-                    if (T.steps >= W.budget && rtk::travc_parkable(T)) {
-                        const int slot = __atomic_fetch_add(&parkc[par ^ 1], 1, __ATOMIC_RELAXED);
-                        if (slot < W.park_cap) {
-                            rtk::travc_park(T, stk, target, &W.park_c[par ^ 1][slot]);
-                            if (!resumed) __atomic_fetch_add(&W.r_park[target >> 3], 1, __ATOMIC_RELAXED);
-                            break;
-                        }
-                        T.steps = 0;
-                    }
-                }
-            }
-#pragma omp for schedule(dynamic, 16)
-            for (int idx = 0; idx < na; idx++) {
-                rtk::TravA T;
-                uint32_t target;
-                bool resumed = idx < nra, has;
-                if (resumed) {
-                    target = rtk::trava_resume(&W.park_a[par][idx], T, stk);
-                    has = true;
-                } else {
-                    const rtk::RayRec r = W.fb_a[idx - nra];
-                    target = (rt_asuint(r.o.w) << 3) | rt_asuint(r.d.w);
-                    if (ps) ps->c[RT_STAT_FALLBACK]++;
-                    has = rtk::trava_begin(W.S, T, rtk::v3of(r.o), rtk::v3of(r.d), ps);
-                    if (!has) rtk::finish_any(W, target, false);
-                }
-                while (has) {
-                    if (!rtk::trava_step(W.S, T, stk, ps)) {
-                        rtk::finish_any(W, target, T.hit);
-                        if (resumed) __atomic_fetch_sub(&W.r_park[target >> 3], 1, __ATOMIC_RELAXED);
-                        break;
-                    }
-                    if (T.steps >= W.budget && rtk::trava_parkable(T)) {
-                        const int slot = __atomic_fetch_add(&parka[par ^ 1], 1, __ATOMIC_RELAXED);
-                        if (slot < W.park_cap) {
-                            rtk::trava_park(T, stk, target, &W.park_a[par ^ 1][slot]);
-                            if (!resumed) __atomic_fetch_add(&W.r_park[target >> 3], 1, __ATOMIC_RELAXED);
-                            break;
-                        }
-                        T.steps = 0;
-                    }
-                }
-            }
-        }
+        // k_step
         for (int k = 0; k < rtk::RK_COUNT; k++) counters[k] = 0;
         parkc[par] = parka[par] = 0;
+        fbc[par] = fba[par] = 0;
         act[par ^ 1] = 0;
         W.act_in = lists[par];
         W.act_out = lists[par ^ 1];

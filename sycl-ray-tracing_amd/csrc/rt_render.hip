@@ -39,22 +39,28 @@ struct DevBuf {
     size_t bytes = 0;
 };
 
-// counters[] layout (int32)
+// counters[] layout (int32). Iteration i (p = i & 1) runs k_trace(i) then
+// k_step(i); every set is zeroed by the launch before the one that fills it,
+// so no reset launch is needed:
+//   Q[p]      queue sizes     filled by k_step(i-1) / k_init, read by k_trace(i); k_trace(i) zeroes Q[p^1]
+//   ACT[p]    live count      filled by k_step(i-1) / k_init, read by k_step(i);  k_trace(i) zeroes ACT[p^1]
+//   FB[p]     fallback sizes  filled by k_trace(i-1), read by k_trace(i), which fills FB[p^1]; k_step(i) zeroes FB[p]
+//   PARK[p]   parked queries  likewise
+//   TK        exact-walk work tickets of k_trace(i); k_step(i) zeroes them
 enum {
-    C_Q0 = 0,                 // queue sizes, RK_COUNT entries
-    C_TK_CLOSEST = rtk::RK_COUNT,
-    C_TK_ANY,
-    C_TK_STEP,
-    C_TK_EXACT_C,             // tickets of the exact (fallback) kernels
-    C_TK_EXACT_A,
-    C_FBC,                    // fallback list sizes
-    C_FBA,
-    C_ACT0,                   // live-slot counts, double-buffered
-    C_ACT1,
-    C_PARKC0,                 // parked queries, double-buffered by iteration parity
+    C_Q = 0,  // + set * RK_COUNT + kind
+    C_FBC0 = 2 * rtk::RK_COUNT,
+    C_FBC1,
+    C_FBA0,
+    C_FBA1,
+    C_PARKC0,
     C_PARKC1,
     C_PARKA0,
     C_PARKA1,
+    C_TK_EXACT_C,
+    C_TK_EXACT_A,
+    C_ACT0,
+    C_ACT1,
     C_COUNT
 };
 
@@ -74,8 +80,8 @@ struct Backend {
     int budget = 1024;  // steps per query per launch before it parks (RT_STEP_BUDGET)
     // optional per-kernel timing: events around each launch of each class
     bool timing = false;
-    hipEvent_t tev[4][RT_MAX_TIMED_ITERS] = {};
-    double kms[3] = {0, 0, 0};      // closest, any, step
+    hipEvent_t tev[3][RT_MAX_TIMED_ITERS] = {};
+    double kms[3] = {0, 0, 0};      // k_trace, k_step, (unused)
     long klaunch[3] = {0, 0, 0};
 };
 
@@ -135,8 +141,6 @@ struct LdsStack {
     }
     __device__ __forceinline__ void set_rec(int i, uint32_t rv) { r[i * 256] = rv; }
 };
-#define RT_LDS_CAP_CLOSEST 16
-#define RT_LDS_CAP_ANY 16
 
 // Static wave-strided work assignment: wave w of the grid takes items
 // [w*64, w*64+64), then strides by the grid's wave count. (A shared atomic
@@ -144,14 +148,6 @@ struct LdsStack {
 // ~45 us even for an empty queue.)
 __device__ __forceinline__ int wave_gid() { return (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6); }
 __device__ __forceinline__ int wave_count() { return (int)((gridDim.x * blockDim.x) >> 6); }
-
-// One ticket of 64 work items per wave.
-__device__ __forceinline__ int wave_ticket(int32_t* ticket)
-{
-    int base = 0;
-    if (lane_id() == 0) base = atomicAdd(ticket, 64);
-    return __shfl(base, 0);
-}
 
 template <bool STATS>
 __device__ __forceinline__ void flush_stats(const rtk::Stats& st, unsigned long long* out)
@@ -162,29 +158,41 @@ __device__ __forceinline__ void flush_stats(const rtk::Stats& st, unsigned long 
 }
 
 // ------------------------------------------------------------------ kernels
-// Path init: every slot seeds its RNG and emits its first camera ray.
-__global__ __launch_bounds__(256) void k_init(rtk::WaveView W, int32_t* act_count)
+__device__ __forceinline__ void append_emit(const rtk::WaveView& W, int32_t* qcount, int32_t* act_count, int p,
+                                            const rtk::Emit& e)
 {
-    const int p = blockIdx.x * blockDim.x + threadIdx.x;  // grid covers whole waves
-    rtk::Emit e;
-    e.mask = 0;
-    e.active = false;
-    if (p < W.n_slots) rtk::path_init(W, p, e);
 #pragma unroll
     for (int k = 0; k < rtk::RK_COUNT; k++) {
         const bool want = (e.mask >> k) & 1u;
-        const int i = wave_append(W.counters + C_Q0 + k, want);
+        const int i = wave_append(qcount + k, want);
         if (want) W.q[k][i] = e.r[k];
     }
     const int a = wave_append(act_count, e.active);
     if (e.active) W.act_out[a] = p;
 }
 
-template <bool STATS>
-__global__ __launch_bounds__(256, 3) void k_step(rtk::WaveView W, const int32_t* act_in_count, int32_t* act_out_count,
-                                              unsigned long long* stats)
+// Path init: every slot seeds its RNG and emits its first camera ray (into Q[0], ACT[0]).
+__global__ __launch_bounds__(256) void k_init(rtk::WaveView W)
 {
-    const int n = *act_in_count;
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;  // grid covers whole waves
+    rtk::Emit e;
+    e.mask = 0;
+    e.active = false;
+    if (p < W.n_slots) rtk::path_init(W, p, e);
+    append_emit(W, W.counters + C_Q, W.counters + C_ACT0, p, e);
+}
+
+template <bool STATS>
+__global__ __launch_bounds__(256, 3) void k_step(rtk::WaveView W, int par, unsigned long long* stats)
+{
+    int32_t* cnt = W.counters;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {  // read by k_trace(i); refilled by k_trace(i + 1)
+        cnt[C_FBC0 + par] = cnt[C_FBA0 + par] = cnt[C_PARKC0 + par] = cnt[C_PARKA0 + par] = 0;
+        cnt[C_TK_EXACT_C] = cnt[C_TK_EXACT_A] = 0;
+    }
+    const int n = cnt[C_ACT0 + par];
+    int32_t* qout = cnt + C_Q + (par ^ 1) * rtk::RK_COUNT;
+    int32_t* aout = cnt + C_ACT0 + (par ^ 1);
     rtk::Stats st;
     if (STATS)
         for (int i = 0; i < RT_STAT_COUNT; i++) st.c[i] = 0;
@@ -198,24 +206,31 @@ __global__ __launch_bounds__(256, 3) void k_step(rtk::WaveView W, const int32_t*
             p = W.act_in[idx];
             rtk::path_step(W, p, e, STATS ? &st : nullptr);
         }
-#pragma unroll
-        for (int k = 0; k < rtk::RK_COUNT; k++) {
-            const bool want = (e.mask >> k) & 1u;
-            const int i = wave_append(W.counters + C_Q0 + k, want);
-            if (want) W.q[k][i] = e.r[k];
-        }
-        const int a = wave_append(act_out_count, e.active);
-        if (e.active) W.act_out[a] = p;
+        append_emit(W, qout, aout, p, e);
     }
     flush_stats<STATS>(st, stats);
 }
 
-// -------------------------------------------------------- fast query kernels
-// One query per lane at a time through the search BVH (rt_fast.h), stack of
-// node indices in LDS; a query whose answer needs the exact octree walk (or
-// whose stack would overflow) goes to the fallback list for
-// k_exact_closest / k_exact_any.
+// ------------------------------------------------------------- query kernel
+// Every closest-hit and occlusion query of the iteration, plus the exact
+// octree walks of the queries the previous iteration could not settle, in
+// one launch: the blocks are split into four roles computed alike by every
+// block from the counters.
+//  * exact roles (blocks first, so their long dependent walks start early
+//    and hide under the bulk): the previous launch's fallback lists and
+//    parked walks, through the resumable octree walk (rt_traverse.h).
+//    Persistent waves; idle lanes refill once RT_REFILL of them are idle; a
+//    walk that has taken W.budget steps parks at its next node boundary and
+//    continues in the next launch.
+//  * fast roles (the rest, split in proportion to the two queues): one query
+//    per lane through the search BVH (rt_fast.h), node-index stack in LDS. A
+//    query whose answer needs the exact walk (or whose stack would overflow)
+//    goes to the fallback list for the next launch, and its slot's r_park
+//    count keeps k_step off the path until the walk has finished.
 #define RT_LDS_CAP_FAST 24
+#define RT_LDS_CAP_CLOSEST 8  // key + record: 16 of the 24 words per lane (windows are powers of two)
+#define RT_LDS_CAP_ANY 16
+#define RT_REFILL 16
 
 template <int N>
 struct LdsIdx {
@@ -225,97 +240,25 @@ struct LdsIdx {
     __device__ __forceinline__ void set_rec(int i, uint32_t v) { r[i * 256] = v; }
 };
 
-template <bool STATS>
-__global__ __launch_bounds__(256, 6) void k_fast_closest(rtk::WaveView W, unsigned long long* stats)
+// Blocks [0, n0) take role 0, the rest role 1, in proportion to the work.
+__device__ __forceinline__ int split_blocks(int nb, int w0, int w1)
 {
-    __shared__ uint32_t s_r[RT_LDS_CAP_FAST * 256];
-    LdsIdx<RT_LDS_CAP_FAST> stk{s_r + threadIdx.x};
-    const int last_kind = W.any_rays ? rtk::RK_BL : rtk::RK_BENV;
-    int total = 0;
-    for (int k = rtk::RK_CONT; k <= last_kind; k++) total += W.counters[C_Q0 + k];
-    rtk::Stats st;
-    if (STATS)
-        for (int i = 0; i < RT_STAT_COUNT; i++) st.c[i] = 0;
-    for (int base = wave_gid() * 64; base < total; base += wave_count() * 64) {
-        const int idx = base + lane_id();
-        bool fail = false;
-        rtk::RayRec r;
-        uint32_t target = 0;
-        if (idx < total) {
-            r = rtk::queue_item(W, W.counters + C_Q0, rtk::RK_CONT, last_kind, idx, target);
-            float t;
-            int k;
-            if (rtk::fast_query_closest(W.S, rtk::v3of(r.o), rtk::v3of(r.d), stk, t, k, STATS ? &st : nullptr))
-                rtk::finish_closest(W, target, rtk::v3of(r.o), rtk::v3of(r.d), t, k);
-            else
-                fail = true;
-        }
-        const int f = wave_append(W.counters + C_FBC, fail);
-        if (fail) {
-            r.d.w = rt_asfloat(target & 7u);
-            W.fb_c[f] = r;
-        }
-    }
-    flush_stats<STATS>(st, stats);
+    if (w0 + w1 == 0) return 0;
+    int n0 = (int)((long)nb * w0 / ((long)w0 + w1));
+    if (w0 > 0 && n0 == 0) n0 = 1;
+    if (w1 > 0 && n0 == nb) n0 = nb - 1;
+    return n0;
 }
 
-template <bool STATS>
-__global__ __launch_bounds__(256, 6) void k_fast_any(rtk::WaveView W, unsigned long long* stats)
+__device__ void exact_closest(const rtk::WaveView& W, int par, uint32_t* lds, int lane, int n_res, int total,
+                              rtk::Stats* st)
 {
-    __shared__ uint32_t s_r[RT_LDS_CAP_FAST * 256];
-    LdsIdx<RT_LDS_CAP_FAST> stk{s_r + threadIdx.x};
-    const int total = W.counters[C_Q0 + rtk::RK_ESH] + W.counters[C_Q0 + rtk::RK_BENV];
-    rtk::Stats st;
-    if (STATS)
-        for (int i = 0; i < RT_STAT_COUNT; i++) st.c[i] = 0;
-    for (int base = wave_gid() * 64; base < total; base += wave_count() * 64) {
-        const int idx = base + lane_id();
-        bool fail = false;
-        rtk::RayRec r;
-        uint32_t target = 0;
-        if (idx < total) {
-            r = rtk::queue_item(W, W.counters + C_Q0, rtk::RK_ESH, rtk::RK_BENV, idx, target);
-            const int a = rtk::fast_query_any(W.S, rtk::v3of(r.o), rtk::v3of(r.d), stk, STATS ? &st : nullptr);
-            if (a >= 0)
-                rtk::finish_any(W, target, a == 1);
-            else
-                fail = true;
-        }
-        const int f = wave_append(W.counters + C_FBA, fail);
-        if (fail) {
-            r.d.w = rt_asfloat(target & 7u);
-            W.fb_a[f] = r;
-        }
-    }
-    flush_stats<STATS>(st, stats);
-}
-
-// ------------------------------------------------------- exact (fallback) kernels
-// Persistent waves; each lane runs one query at a time, one unit of work per
-// loop trip (rt_traverse.h). Idle lanes refill from the work list (parked
-// queries of the last launch first, then the queues) once REFILL lanes are
-// idle; a query that has taken W.budget steps parks at its next node
-// boundary. Work list order: parked, then the ray kinds in queue order.
-#define RT_REFILL 16
-
-template <bool STATS>
-__global__ __launch_bounds__(256, 4) void k_exact_closest(rtk::WaveView W, unsigned long long* stats)
-{
-    __shared__ uint32_t s_r[RT_LDS_CAP_CLOSEST * 256];
-    __shared__ float s_k[RT_LDS_CAP_CLOSEST * 256];
     using FAST = LdsStack<RT_LDS_CAP_CLOSEST>;
-    const int gl = blockIdx.x * blockDim.x + threadIdx.x;
-    rtk::SpillStack<FAST> stk{FAST{s_r + threadIdx.x, s_k + threadIdx.x}, W.spill_r + (size_t)gl * RT_STACK_CAP,
-                              W.spill_k + (size_t)gl * RT_STACK_CAP};
-    const int par = W.park_par;
-    const int n_res = min(W.counters[C_PARKC0 + par], W.park_cap);
-    const int total = n_res + W.counters[C_FBC];
-    if (total == 0) return;
-    rtk::Stats st;
-    if (STATS)
-        for (int i = 0; i < RT_STAT_COUNT; i++) st.c[i] = 0;
+    rtk::SpillStack<FAST> stk{FAST{lds + threadIdx.x, (float*)lds + RT_LDS_CAP_CLOSEST * 256 + threadIdx.x},
+                              W.spill_r + (size_t)lane * RT_STACK_CAP, W.spill_k + (size_t)lane * RT_STACK_CAP};
+    const rtk::RayRec* fb = W.fb_c[par];
     rtk::TravC T;
-    bool has = false, resumed = false, drained = false;
+    bool has = false, drained = false;
     uint32_t target = 0;
     for (;;) {
         const bool need = !has;
@@ -330,14 +273,16 @@ __global__ __launch_bounds__(256, 4) void k_exact_closest(rtk::WaveView W, unsig
                 const int idx = base + __popcll(bneed & ((1ull << lane_id()) - 1ull));
                 if (idx < n_res) {
                     target = rtk::travc_resume(&W.park_c[par][idx], T, stk);
-                    has = resumed = true;
+                    has = true;
                 } else if (idx < total) {
-                    const rtk::RayRec r = W.fb_c[idx - n_res];
+                    const rtk::RayRec r = fb[idx - n_res];
                     target = (rt_asuint(r.o.w) << 3) | rt_asuint(r.d.w);
-                    resumed = false;
-                    if (STATS) st.c[RT_STAT_FALLBACK]++;
-                    has = rtk::travc_begin(W.S, T, rtk::v3of(r.o), rtk::v3of(r.d), STATS ? &st : nullptr);
-                    if (!has) rtk::finish_closest(W, target, T.o, T.d, T.best_t, T.best_k);
+                    if (st) st->c[RT_STAT_FALLBACK]++;
+                    has = rtk::travc_begin(W.S, T, rtk::v3of(r.o), rtk::v3of(r.d), st);
+                    if (!has) {
+                        rtk::finish_closest(W, target, T.o, T.d, T.best_t, T.best_k);
+                        atomicSub(&W.r_park[target >> 3], 1);
+                    }
                 }
             }
         }
@@ -346,15 +291,14 @@ __global__ __launch_bounds__(256, 4) void k_exact_closest(rtk::WaveView W, unsig
             continue;
         }
         if (has) {
-            if (!rtk::travc_step(W.S, T, stk, STATS ? &st : nullptr)) {
+            if (!rtk::travc_step(W.S, T, stk, st)) {
                 rtk::finish_closest(W, target, T.o, T.d, T.best_t, T.best_k);
-                if (resumed) atomicSub(&W.r_park[target >> 3], 1);
+                atomicSub(&W.r_park[target >> 3], 1);
                 has = false;
             } else if (T.steps >= W.budget && rtk::travc_parkable(T)) {
                 const int ps = atomicAdd(W.counters + C_PARKC0 + (par ^ 1), 1);
                 if (ps < W.park_cap) {
                     rtk::travc_park(T, stk, target, &W.park_c[par ^ 1][ps]);
-                    if (!resumed) atomicAdd(&W.r_park[target >> 3], 1);
                     has = false;
                 } else {
                     T.steps = 0;  // park pool full: keep going
@@ -362,25 +306,16 @@ __global__ __launch_bounds__(256, 4) void k_exact_closest(rtk::WaveView W, unsig
             }
         }
     }
-    flush_stats<STATS>(st, stats);
 }
 
-template <bool STATS>
-__global__ __launch_bounds__(256, 4) void k_exact_any(rtk::WaveView W, unsigned long long* stats)
+__device__ void exact_any(const rtk::WaveView& W, int par, uint32_t* lds, int lane, int n_res, int total,
+                          rtk::Stats* st)
 {
-    __shared__ uint32_t s_r[RT_LDS_CAP_ANY * 256];
     using FAST = LdsStack<RT_LDS_CAP_ANY>;
-    const int gl = blockIdx.x * blockDim.x + threadIdx.x;
-    rtk::SpillStack<FAST> stk{FAST{s_r + threadIdx.x, nullptr}, W.spill_r + (size_t)gl * RT_STACK_CAP, nullptr};
-    const int par = W.park_par;
-    const int n_res = min(W.counters[C_PARKA0 + par], W.park_cap);
-    const int total = n_res + W.counters[C_FBA];
-    if (total == 0) return;
-    rtk::Stats st;
-    if (STATS)
-        for (int i = 0; i < RT_STAT_COUNT; i++) st.c[i] = 0;
+    rtk::SpillStack<FAST> stk{FAST{lds + threadIdx.x, nullptr}, W.spill_r + (size_t)lane * RT_STACK_CAP, nullptr};
+    const rtk::RayRec* fb = W.fb_a[par];
     rtk::TravA T;
-    bool has = false, resumed = false, drained = false;
+    bool has = false, drained = false;
     uint32_t target = 0;
     for (;;) {
         const bool need = !has;
@@ -395,14 +330,16 @@ __global__ __launch_bounds__(256, 4) void k_exact_any(rtk::WaveView W, unsigned 
                 const int idx = base + __popcll(bneed & ((1ull << lane_id()) - 1ull));
                 if (idx < n_res) {
                     target = rtk::trava_resume(&W.park_a[par][idx], T, stk);
-                    has = resumed = true;
+                    has = true;
                 } else if (idx < total) {
-                    const rtk::RayRec r = W.fb_a[idx - n_res];
+                    const rtk::RayRec r = fb[idx - n_res];
                     target = (rt_asuint(r.o.w) << 3) | rt_asuint(r.d.w);
-                    resumed = false;
-                    if (STATS) st.c[RT_STAT_FALLBACK]++;
-                    has = rtk::trava_begin(W.S, T, rtk::v3of(r.o), rtk::v3of(r.d), STATS ? &st : nullptr);
-                    if (!has) rtk::finish_any(W, target, false);
+                    if (st) st->c[RT_STAT_FALLBACK]++;
+                    has = rtk::trava_begin(W.S, T, rtk::v3of(r.o), rtk::v3of(r.d), st);
+                    if (!has) {
+                        rtk::finish_any(W, target, false);
+                        atomicSub(&W.r_park[target >> 3], 1);
+                    }
                 }
             }
         }
@@ -411,15 +348,14 @@ __global__ __launch_bounds__(256, 4) void k_exact_any(rtk::WaveView W, unsigned 
             continue;
         }
         if (has) {
-            if (!rtk::trava_step(W.S, T, stk, STATS ? &st : nullptr)) {
+            if (!rtk::trava_step(W.S, T, stk, st)) {
                 rtk::finish_any(W, target, T.hit);
-                if (resumed) atomicSub(&W.r_park[target >> 3], 1);
+                atomicSub(&W.r_park[target >> 3], 1);
                 has = false;
             } else if (T.steps >= W.budget && rtk::trava_parkable(T)) {
                 const int ps = atomicAdd(W.counters + C_PARKA0 + (par ^ 1), 1);
                 if (ps < W.park_cap) {
                     rtk::trava_park(T, stk, target, &W.park_a[par ^ 1][ps]);
-                    if (!resumed) atomicAdd(&W.r_park[target >> 3], 1);
                     has = false;
                 } else {
                     T.steps = 0;
@@ -427,19 +363,88 @@ __global__ __launch_bounds__(256, 4) void k_exact_any(rtk::WaveView W, unsigned 
             }
         }
     }
-    flush_stats<STATS>(st, stats);
 }
 
-// Between the trace launches and the step of an iteration: queue sizes and
-// tickets, the live count the step will write, and the park counts the
-// trace launches just consumed.
-__global__ void k_reset(int32_t* counters, int act_slot, int park_par)
+template <bool STATS>
+__global__ __launch_bounds__(256, 6) void k_trace(rtk::WaveView W, int par, unsigned long long* stats)
 {
-    const int i = threadIdx.x;
-    if (i < C_ACT0) counters[i] = 0;
-    if (i == 0) counters[act_slot] = 0;
-    if (i == 1) counters[C_PARKC0 + park_par] = 0;
-    if (i == 2) counters[C_PARKA0 + park_par] = 0;
+    __shared__ uint32_t s_lds[RT_LDS_CAP_FAST * 256];
+    int32_t* cnt = W.counters;
+    const int32_t* q = cnt + C_Q + par * rtk::RK_COUNT;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {  // filled by k_step(i) next
+        for (int k = 0; k < rtk::RK_COUNT; k++) cnt[C_Q + (par ^ 1) * rtk::RK_COUNT + k] = 0;
+        cnt[C_ACT0 + (par ^ 1)] = 0;
+    }
+    rtk::Stats st;
+    if (STATS)
+        for (int i = 0; i < RT_STAT_COUNT; i++) st.c[i] = 0;
+    rtk::Stats* ps = STATS ? &st : nullptr;
+
+    // exact roles: 64 walks per block to start with (16 per wave), at most
+    // half of the spill lanes each
+    const int nrc = min(cnt[C_PARKC0 + par], W.park_cap), nra = min(cnt[C_PARKA0 + par], W.park_cap);
+    const int ec = nrc + cnt[C_FBC0 + par], ea = nra + cnt[C_FBA0 + par];
+    const int half = W.spill_lanes / 512;
+    const int nbe_c = min(half, (ec + 63) / 64), nbe_a = min(half, (ea + 63) / 64);
+    const int b = (int)blockIdx.x;
+    if (b < nbe_c) {
+        exact_closest(W, par, s_lds, b * 256 + (int)threadIdx.x, nrc, ec, ps);
+        flush_stats<STATS>(st, stats);
+        return;
+    }
+    if (b < nbe_c + nbe_a) {
+        exact_any(W, par, s_lds, (half + b - nbe_c) * 256 + (int)threadIdx.x, nra, ea, ps);
+        flush_stats<STATS>(st, stats);
+        return;
+    }
+
+    // fast roles
+    LdsIdx<RT_LDS_CAP_FAST> stk{s_lds + threadIdx.x};
+    const int last_kind = W.any_rays ? rtk::RK_BL : rtk::RK_BENV;
+    int nc = 0;
+    for (int k = rtk::RK_CONT; k <= last_kind; k++) nc += q[k];
+    const int na = W.any_rays ? q[rtk::RK_ESH] + q[rtk::RK_BENV] : 0;
+    const int fb0 = nbe_c + nbe_a, nbf = (int)gridDim.x - fb0;
+    const int nbc = split_blocks(nbf, nc, na);
+    const bool closest = b - fb0 < nbc;
+    const int rb = closest ? b - fb0 : b - fb0 - nbc;                       // block index within the role
+    const int rnb = closest ? nbc : nbf - nbc;                              // blocks of the role
+    const int wg = rb * (int)(blockDim.x >> 6) + (int)(threadIdx.x >> 6);  // wave index within the role
+    const int wn = rnb * (int)(blockDim.x >> 6);
+    const int total = closest ? nc : na;
+    int32_t* fbn = cnt + (closest ? C_FBC0 : C_FBA0) + (par ^ 1);
+    rtk::RayRec* fbl = closest ? W.fb_c[par ^ 1] : W.fb_a[par ^ 1];
+    for (int base = wg * 64; base < total; base += wn * 64) {
+        const int idx = base + lane_id();
+        bool fail = false;
+        rtk::RayRec r;
+        uint32_t target = 0;
+        if (idx < total) {
+            if (closest) {
+                r = rtk::queue_item(W, q, rtk::RK_CONT, last_kind, idx, target);
+                float t;
+                int k;
+                if (rtk::fast_query_closest(W.S, rtk::v3of(r.o), rtk::v3of(r.d), stk, t, k, ps))
+                    rtk::finish_closest(W, target, rtk::v3of(r.o), rtk::v3of(r.d), t, k);
+                else
+                    fail = true;
+            } else {
+                r = rtk::queue_item(W, q, rtk::RK_ESH, rtk::RK_BENV, idx, target);
+                const int a = rtk::fast_query_any(W.S, rtk::v3of(r.o), rtk::v3of(r.d), stk, ps);
+                if (a >= 0)
+                    rtk::finish_any(W, target, a == 1);
+                else
+                    fail = true;
+            }
+        }
+        const int f = wave_append(fbn, fail);
+        if (fail) {
+            r.d.w = rt_asfloat(target & 7u);
+            fbl[f] = r;
+            atomicAdd(&W.r_park[target >> 3], 1);
+        }
+    }
+    flush_stats<STATS>(st, stats);
 }
 
 __global__ __launch_bounds__(256) void k_intersect(RtSceneView S, const float* __restrict__ rays, int32_t* __restrict__ out,
@@ -590,11 +595,10 @@ static int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounce
     (void)hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, c->device);
     const int threads = 256;
     const int step_blocks = std::min((n + threads - 1) / threads, dev_cus * 8);
-    const int trace_blocks = dev_cus * 4;  // exact kernels: persistent, 4 blocks of 256 per CU
-    const int fast_blocks = dev_cus * 8;   // fast kernels: wave-strided; 5 blocks (32 KB LDS each) resident per CU
+    const int trace_blocks = dev_cus * 8;  // k_trace: wave-strided; 6 blocks (24 KB LDS each) resident per CU
     rtk::WaveView W{};
     W.park_cap = 1 << 16;
-    W.spill_lanes = trace_blocks * threads;
+    W.spill_lanes = dev_cus * 4 * threads;  // exact walks: up to dev_cus * 2 blocks per role
     const size_t need = rtk::wave_carve(nullptr, (size_t)n, W);
     if (int r = ensure(c, b->wave, need)) return r;
     rtk::wave_carve((char*)b->wave.p, (size_t)n, W);
@@ -624,54 +628,40 @@ static int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounce
     HIPCHK(c, hipMemsetAsync(W.r_park, 0, (size_t)n * 4, s));
     W.act_in = lists[1];
     W.act_out = lists[0];
-    hipLaunchKernelGGL(k_init, dim3((n + threads - 1) / threads), dim3(threads), 0, s, W, cnt + C_ACT0);
+    hipLaunchKernelGGL(k_init, dim3((n + threads - 1) / threads), dim3(threads), 0, s, W);
     HIPCHK(c, hipGetLastError());
 
-    // A sample takes at most bounces + 1 iterations without parking; parked
-    // queries stretch that. The bound only guards against a runaway loop.
+    // Two launches per iteration (k_trace, k_step); the counter sets they
+    // fill are double-buffered by iteration parity (see C_Q).
+    // A sample takes at most bounces + 1 iterations without fallbacks; an
+    // exact walk delays its path by at least one iteration. The bound only
+    // guards against a runaway loop.
     const long max_iters = 64l * spp * ((long)bounces + 1) + 4096;
     int it = 0;
     bool done = false;
     for (; it < max_iters && !done; it++) {
-        const int cur = it & 1;
+        const int par = it & 1;
         const bool T = b->timing && it < RT_MAX_TIMED_ITERS;
         if (T)
-            for (int k = 0; k < 4; k++)
+            for (int k = 0; k < 3; k++)
                 if (!b->tev[k][it]) HIPCHK(c, hipEventCreate(&b->tev[k][it]));
-        W.park_par = cur;
+        // step: reads the list written last iteration (lists[par]) -> lists[par ^ 1]
+        W.act_in = lists[par];
+        W.act_out = lists[par ^ 1];
         if (T) HIPCHK(c, hipEventRecord(b->tev[0][it], s));
-        if (S) {
-            hipLaunchKernelGGL(k_fast_closest<true>, dim3(fast_blocks), dim3(threads), 0, s, W, stats);
-            hipLaunchKernelGGL(k_exact_closest<true>, dim3(trace_blocks), dim3(threads), 0, s, W, stats);
-        } else {
-            hipLaunchKernelGGL(k_fast_closest<false>, dim3(fast_blocks), dim3(threads), 0, s, W, stats);
-            hipLaunchKernelGGL(k_exact_closest<false>, dim3(trace_blocks), dim3(threads), 0, s, W, stats);
-        }
-        if (T) HIPCHK(c, hipEventRecord(b->tev[1][it], s));
-        if (W.any_rays) {
-            if (S) {
-                hipLaunchKernelGGL(k_fast_any<true>, dim3(fast_blocks), dim3(threads), 0, s, W, stats);
-                hipLaunchKernelGGL(k_exact_any<true>, dim3(trace_blocks), dim3(threads), 0, s, W, stats);
-            } else {
-                hipLaunchKernelGGL(k_fast_any<false>, dim3(fast_blocks), dim3(threads), 0, s, W, stats);
-                hipLaunchKernelGGL(k_exact_any<false>, dim3(trace_blocks), dim3(threads), 0, s, W, stats);
-            }
-        }
-        if (T) HIPCHK(c, hipEventRecord(b->tev[2][it], s));
-        hipLaunchKernelGGL(k_reset, dim3(1), dim3(64), 0, s, cnt, C_ACT0 + (cur ^ 1), cur);
-        // step: reads the list written last iteration (lists[cur]) -> lists[cur ^ 1]
-        W.act_in = lists[cur];
-        W.act_out = lists[cur ^ 1];
         if (S)
-            hipLaunchKernelGGL(k_step<true>, dim3(step_blocks), dim3(threads), 0, s, W, cnt + C_ACT0 + cur,
-                               cnt + C_ACT0 + (cur ^ 1), stats);
+            hipLaunchKernelGGL(k_trace<true>, dim3(trace_blocks), dim3(threads), 0, s, W, par, stats);
         else
-            hipLaunchKernelGGL(k_step<false>, dim3(step_blocks), dim3(threads), 0, s, W, cnt + C_ACT0 + cur,
-                               cnt + C_ACT0 + (cur ^ 1), stats);
-        if (T) HIPCHK(c, hipEventRecord(b->tev[3][it], s));
+            hipLaunchKernelGGL(k_trace<false>, dim3(trace_blocks), dim3(threads), 0, s, W, par, stats);
+        if (T) HIPCHK(c, hipEventRecord(b->tev[1][it], s));
+        if (S)
+            hipLaunchKernelGGL(k_step<true>, dim3(step_blocks), dim3(threads), 0, s, W, par, stats);
+        else
+            hipLaunchKernelGGL(k_step<false>, dim3(step_blocks), dim3(threads), 0, s, W, par, stats);
+        if (T) HIPCHK(c, hipEventRecord(b->tev[2][it], s));
         HIPCHK(c, hipGetLastError());
         if ((it & 7) == 7) {
-            HIPCHK(c, hipMemcpyAsync(b->h_act, cnt + C_ACT0 + (cur ^ 1), 4, hipMemcpyDeviceToHost, s));
+            HIPCHK(c, hipMemcpyAsync(b->h_act, cnt + C_ACT0 + (par ^ 1), 4, hipMemcpyDeviceToHost, s));
             HIPCHK(c, hipStreamSynchronize(s));
             done = *b->h_act == 0;
         }
@@ -684,7 +674,7 @@ static int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounce
     if (b->timing) {  // per-kernel-class time of this render (HIP events on its stream)
         HIPCHK(c, hipStreamSynchronize(s));
         for (int i = 0; i < b->last_iters && i < RT_MAX_TIMED_ITERS; i++)
-            for (int k = 0; k < 3; k++) {
+            for (int k = 0; k < 2; k++) {
                 float ms = 0;
                 HIPCHK(c, hipEventElapsedTime(&ms, b->tev[k][i], b->tev[k + 1][i]));
                 b->kms[k] += ms;
@@ -809,7 +799,7 @@ extern "C" double rt_device_last_kernel_ms(rt_context* c)
 // Iterations the last wavefront render took.
 extern "C" int rt_device_last_iterations(rt_context* c) { return c && c->backend ? be(c)->last_iters : -1; }
 
-// Per-kernel-class timing (closest-hit trace, occlusion trace, step) over
+// Per-kernel-class timing (k_trace, k_step, reserved) over
 // the renders since it was enabled: out_ms[3] total ms, out_launches[3].
 extern "C" int rt_device_kernel_timing(rt_context* c, int enable, double* out_ms, long* out_launches)
 {

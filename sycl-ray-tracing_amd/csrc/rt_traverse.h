@@ -35,6 +35,7 @@ struct SpillStack {
     float* spill_k;     // (unused by the occlusion walk)
     static constexpr int CAP = FAST::CAP;
     static constexpr int MASK = CAP - 1;
+    static_assert(CAP >= 8 && (CAP & MASK) == 0, "the window is a ring: CAP must be a power of two >= 8");
     RT_HD uint32_t rec(int i, int lo) const { return i >= lo ? f.rec(i & MASK) : spill_r[i]; }
     RT_HD float key(int i, int lo) const { return i >= lo ? f.key(i & MASK) : spill_k[i]; }
 };

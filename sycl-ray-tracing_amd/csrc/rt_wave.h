@@ -98,12 +98,11 @@ struct WaveView {
     RayRec* q[RK_COUNT];    // [n_slots] each
     int32_t* counters;      // queue sizes, tickets, live counts (rt_render.hip C_*)
     int32_t* r_park;        // [n_slots] queries of the slot parked (the step skips the slot while > 0)
-    RayRec* fb_c;           // [5 n_slots] closest-hit queries left to the exact walk (d.w = kind)
-    RayRec* fb_a;           // [2 n_slots] occlusion queries left to the exact walk
+    RayRec* fb_c[2];        // [5 n_slots] closest-hit queries left to the exact walk (d.w = kind), by parity
+    RayRec* fb_a[2];        // [2 n_slots] occlusion queries left to the exact walk, by parity
     ParkC* park_c[2];       // parked closest-hit queries, double-buffered by iteration parity
     ParkA* park_a[2];
     int park_cap;
-    int park_par;           // parity this iteration reads
     int budget;             // steps a query may take per launch before it parks
     uint32_t* spill_r;      // per-lane stack spill areas of the trace kernels
     float* spill_k;
@@ -148,9 +147,9 @@ inline size_t wave_carve(char* base, size_t n, WaveView& W)  // uses W.park_cap,
     W.act_in = (const int32_t*)take(n * 4);
     W.act_out = (int32_t*)take(n * 4);
     W.r_park = (int32_t*)take(n * 4);
-    W.fb_c = (RayRec*)take(5 * n * sizeof(RayRec));
-    W.fb_a = (RayRec*)take(2 * n * sizeof(RayRec));
     for (int k = 0; k < 2; k++) {
+        W.fb_c[k] = (RayRec*)take(5 * n * sizeof(RayRec));
+        W.fb_a[k] = (RayRec*)take(2 * n * sizeof(RayRec));
         W.park_c[k] = (ParkC*)take((size_t)W.park_cap * sizeof(ParkC));
         W.park_a[k] = (ParkA*)take((size_t)W.park_cap * sizeof(ParkA));
     }

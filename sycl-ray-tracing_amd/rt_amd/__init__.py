@@ -239,12 +239,13 @@ class RenderKernel:
     def kernel_timing(self, enable: int = -1):
         """Per-kernel-class GPU time (HIP events around every launch) since
         timing was last enabled: {class: (total_ms, launches)} for the
-        closest-hit trace, occlusion trace and step kernels. enable=1/0
+        query kernel (k_trace, with its exact-walk role) and the path step
+        (k_step); "other" is reserved. enable=1/0
         turns timing on/off and resets the totals; -1 only reads."""
         ms = np.zeros(3, dtype=np.float64)
         n = np.zeros(3, dtype=np.int64)
         check(self.L, self.L.rt_device_kernel_timing(self.ctx, enable, ptr(ms), ptr(n)), self.ctx, "kernel_timing")
-        return {k: (float(a), int(b)) for k, a, b in zip(("trace_closest", "trace_any", "step"), ms, n)}
+        return {k: (float(a), int(b)) for k, a, b in zip(("trace", "step", "other"), ms, n)}
 
     def last_iterations(self) -> int:
         return int(self.L.rt_device_last_iterations(self.ctx))
