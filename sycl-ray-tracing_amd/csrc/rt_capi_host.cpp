@@ -46,7 +46,7 @@ RtSceneView rt_host_view(const rt_context* c)
     v.eh = c->eh;
     v.n_tris = (int)(c->tris.size() / 9);
     v.chain_monotone = c->flat.chain_monotone ? 1 : 0;
-    v.bvh = c->flat.bvh.data();
+    v.bvh4 = c->flat.bvh4.data();
     v.bvh_tri4 = c->flat.bvh_tri4.data();
     v.parent = c->flat.parent.data();
     v.leaf_of = c->flat.leaf_of.data();
@@ -190,7 +190,7 @@ int rt_bvh_info(const rt_context* c, long* info)
     info[3] = c->flat.max_depth;
     info[4] = (long)(c->flat.nodes.size() * sizeof(RtNode) + c->flat.tri4.size() * sizeof(float4_) +
                      c->flat.prim2k.size() * 4 + c->flat.parent.size() * 4 + c->flat.leaf_of.size() * 4 +
-                     c->flat.bvh.size() * sizeof(BvhNode) + c->flat.bvh_tri4.size() * sizeof(float4_));
+                     c->flat.bvh4.size() * sizeof(Bvh4Node) + c->flat.bvh_tri4.size() * sizeof(float4_));
     return RT_OK;
 }
 

@@ -42,6 +42,17 @@ struct alignas(16) BvhNode {
 };
 static_assert(sizeof(BvhNode) == 64, "BvhNode must be 64 B");
 
+// 4-wide search BVH collapsed from the binary one (rt_scene.cpp
+// collapse_bvh4): 128 B = one L2 line; child boxes stored per axis so a
+// node is 8 float4 loads and four slab tests in lock-step. Child c: inner
+// node index (cnt 0), leaf's first entry in bvh_tri4 (cnt 1..4) or nothing
+// (cnt -1, box empty).
+struct alignas(128) Bvh4Node {
+    float lox[4], hix[4], loy[4], hiy[4], loz[4], hiz[4];
+    int32_t ref[4], cnt[4];
+};
+static_assert(sizeof(Bvh4Node) == 128, "Bvh4Node must be 128 B");
+
 struct alignas(16) RtMat {
     float er, eg, eb, metalness;
     float dr, dg, db, roughness;
@@ -63,7 +74,7 @@ struct RtSceneView {
     int32_t n_emissive, n_spheres, ew, eh;
     int32_t n_tris, chain_monotone, cdf_cw, pad2;  // chain_monotone: see rt_fast.h chain_ok
     // search BVH + octree back-links for the verification walk
-    const BvhNode* bvh;        // [0] = root (its two boxes are the scene's halves)
+    const Bvh4Node* bvh4;      // [0] = root
     const float4_* bvh_tri4;   // 3 records per triangle in BVH leaf order: {a.xyz, k}, {e1, leaf record}, {e2}
     const int32_t* parent;     // octree record -> parent record (-1 for the root)
     const int32_t* leaf_of;    // leaf-order triangle k -> its octree leaf record

@@ -63,21 +63,74 @@ RT_HD bool box_hit(const float* mn, const float* mx, const RayB& r, float tmax, 
     return t0 <= t1 && t1 >= 0.0f;
 }
 
-struct BvhNodeR {
-    float lmin[3], lmax[3], rmin[3], rmax[3];
-    int32_t left, right, lcount, rcount;
+struct Bvh4R {
+    float lo[3][4], hi[3][4];
+    int32_t ref[4], cnt[4];
 };
-RT_HD BvhNodeR load_bvh(const BvhNode* nodes, int i)
+RT_HD Bvh4R load_bvh4(const Bvh4Node* nodes, int i)
 {
     const float4_* p = (const float4_*)(nodes + i);
-    const float4_ a = p[0], b = p[1], c = p[2], d = p[3];
-    BvhNodeR n;
-    n.lmin[0] = a.x, n.lmin[1] = a.y, n.lmin[2] = a.z, n.lmax[0] = a.w;
-    n.lmax[1] = b.x, n.lmax[2] = b.y, n.rmin[0] = b.z, n.rmin[1] = b.w;
-    n.rmin[2] = c.x, n.rmax[0] = c.y, n.rmax[1] = c.z, n.rmax[2] = c.w;
-    n.left = (int32_t)rt_asuint(d.x), n.right = (int32_t)rt_asuint(d.y);
-    n.lcount = (int32_t)rt_asuint(d.z), n.rcount = (int32_t)rt_asuint(d.w);
+    float4_ q[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) q[j] = p[j];
+    Bvh4R n;
+#pragma unroll
+    for (int ax = 0; ax < 3; ax++) {
+        const float4_ l = q[2 * ax], h = q[2 * ax + 1];
+        n.lo[ax][0] = l.x, n.lo[ax][1] = l.y, n.lo[ax][2] = l.z, n.lo[ax][3] = l.w;
+        n.hi[ax][0] = h.x, n.hi[ax][1] = h.y, n.hi[ax][2] = h.z, n.hi[ax][3] = h.w;
+    }
+    n.ref[0] = (int32_t)rt_asuint(q[6].x), n.ref[1] = (int32_t)rt_asuint(q[6].y);
+    n.ref[2] = (int32_t)rt_asuint(q[6].z), n.ref[3] = (int32_t)rt_asuint(q[6].w);
+    n.cnt[0] = (int32_t)rt_asuint(q[7].x), n.cnt[1] = (int32_t)rt_asuint(q[7].y);
+    n.cnt[2] = (int32_t)rt_asuint(q[7].z), n.cnt[3] = (int32_t)rt_asuint(q[7].w);
     return n;
+}
+
+// The four child boxes of a node: entry distance and "passes within [0, tmax]".
+RT_HD void box4(const Bvh4R& n, const RayB& r, float tmax, float* tn, bool* hit)
+{
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+        const float mn[3] = {n.lo[0][c], n.lo[1][c], n.lo[2][c]}, mx[3] = {n.hi[0][c], n.hi[1][c], n.hi[2][c]};
+        hit[c] = n.cnt[c] >= 0 && box_hit(mn, mx, r, tmax, tn[c]);
+    }
+}
+
+// A leaf's triangle records (count <= 4, contiguous in bvh_tri4), all
+// loaded before any is tested: one memory round trip per leaf.
+struct LeafTris {
+    float4_ a[4], e1[4], e2[4];
+};
+RT_HD void load_leaf(const RtSceneView& S, int first, int count, LeafTris& L)
+{
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        const int i = first + (j < count ? j : count - 1);
+        L.a[j] = S.bvh_tri4[3 * i];
+        L.e1[j] = S.bvh_tri4[3 * i + 1];
+        L.e2[j] = S.bvh_tri4[3 * i + 2];
+    }
+}
+
+// Sorts four (key, value) pairs by key, ascending (5 compare-exchanges).
+RT_HD void sort4(float* k, int* v)
+{
+    auto cx = [&](int i, int j) {
+        if (k[j] < k[i]) {
+            const float tk = k[i];
+            k[i] = k[j];
+            k[j] = tk;
+            const int tv = v[i];
+            v[i] = v[j];
+            v[j] = tv;
+        }
+    };
+    cx(0, 1);
+    cx(2, 3);
+    cx(0, 2);
+    cx(1, 3);
+    cx(1, 2);
 }
 
 // Relative width of the window past t* in which other hits are collected.
@@ -93,15 +146,18 @@ struct FastHit {
 
 RT_HD void fast_leaf(const RtSceneView& S, int first, int count, V3 o, V3 d, FastHit& h, Stats* st)
 {
-    for (int j = 0; j < count; j++) {
-        const int i = first + j;
+    LeafTris L;
+    load_leaf(S, first, count, L);
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        if (j >= count) break;
         float t;
-        if (tri_test(S.bvh_tri4, i, o, d, t)) {
+        if (tri_test_v(ld3(L.a[j]), ld3(L.e1[j]), ld3(L.e2[j]), o, d, t)) {
             if (t < h.t) {
                 h.t2 = h.t;
                 h.t = t;
-                h.k = (int)rt_asuint(S.bvh_tri4[3 * i].w);
-                h.leaf = (int)rt_asuint(S.bvh_tri4[3 * i + 1].w);
+                h.k = (int)rt_asuint(L.a[j].w);
+                h.leaf = (int)rt_asuint(L.e1[j].w);
                 h.tie = false;
             } else if (t == h.t) {
                 h.tie = true;
@@ -115,7 +171,11 @@ RT_HD void fast_leaf(const RtSceneView& S, int first, int count, V3 o, V3 d, Fas
 }
 
 // All M-T hits within [0, t*(1 + RT_T2_WINDOW)]: closest, tie flag, second.
-// STK: rec(i) / set_rec(i, v) over CAP entries.
+// The result does not depend on the visiting order (every box holding a hit
+// in the final window is entered: the window only shrinks, to the final
+// one), so the walk is free to go nearest-first and to drop stack entries
+// the window has closed behind.
+// STK: CAP entries, rec(i) / key(i) / set(i, rec, key).
 template <class STK>
 RT_HD void fast_closest(const RtSceneView& S, V3 o, V3 d, STK& stk, FastHit& h, Stats* st)
 {
@@ -133,39 +193,48 @@ RT_HD void fast_closest(const RtSceneView& S, V3 o, V3 d, STK& stk, FastHit& h, 
     int sp = 0;
     int cur = 0;
     for (;;) {
-        const BvhNodeR n = load_bvh(S.bvh, cur);
-        if (st) st->c[RT_STAT_VOL] += 2;
-        const float tmax = h.t + h.t * RT_T2_WINDOW;
-        float tl, tr;
-        const bool hl = n.lcount >= 0 && box_hit(n.lmin, n.lmax, rb, tmax, tl);
-        const bool hr = n.rcount >= 0 && box_hit(n.rmin, n.rmax, rb, tmax, tr);
-        int next = -1, far_ = -1;
-        if (hl && n.lcount > 0) fast_leaf(S, n.left, n.lcount, o, d, h, st);
-        if (hr && n.rcount > 0) fast_leaf(S, n.right, n.rcount, o, d, h, st);
-        const bool il = hl && n.lcount == 0, ir = hr && n.rcount == 0;
-        if (il && ir) {
-            const bool lfirst = tl <= tr;
-            next = lfirst ? n.left : n.right;
-            far_ = lfirst ? n.right : n.left;
-        } else if (il) {
-            next = n.left;
-        } else if (ir) {
-            next = n.right;
+        const Bvh4R n = load_bvh4(S.bvh4, cur);
+        if (st) st->c[RT_STAT_VOL] += 4;
+        float tn[4];
+        bool hit[4];
+        box4(n, rb, h.t + h.t * RT_T2_WINDOW, tn, hit);
+#pragma unroll
+        for (int c = 0; c < 4; c++)
+            if (hit[c] && n.cnt[c] > 0) fast_leaf(S, n.ref[c], n.cnt[c], o, d, h, st);
+        const float tmax = h.t + h.t * RT_T2_WINDOW;  // (the leaves may have narrowed it)
+        float k[4];
+        int v[4];
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+            const bool open = hit[c] && n.cnt[c] == 0 && tn[c] <= tmax;
+            k[c] = open ? tn[c] : __builtin_inff();
+            v[c] = open ? n.ref[c] : -1;
         }
-        if (far_ >= 0) {
-            if (sp == STK::CAP) {
-                h.ovf = true;
-                return;
+        sort4(k, v);
+        // far children on the stack (nearest of them on top), nearest next
+#pragma unroll
+        for (int j = 3; j >= 1; j--)
+            if (v[j] >= 0) {
+                if (sp == STK::CAP) {
+                    h.ovf = true;
+                    return;
+                }
+                stk.set(sp++, (uint32_t)v[j], k[j]);
             }
-            stk.set_rec(sp++, (uint32_t)far_);
-        }
-        if (next >= 0) {
-            cur = next;
+        if (v[0] >= 0) {
+            cur = v[0];
             continue;
         }
-        // pop, skipping subtrees the window has closed behind (their boxes are re-tested anyway)
-        if (sp == 0) break;
-        cur = (int)stk.rec(--sp);
+        // pop, dropping entries the window has closed behind
+        cur = -1;
+        while (sp > 0) {
+            --sp;
+            if (stk.key(sp) <= tmax) {
+                cur = (int)stk.rec(sp);
+                break;
+            }
+        }
+        if (cur < 0) break;
     }
     if (h.k < 0) h.t = -1.0f;
 }
@@ -220,7 +289,8 @@ RT_HD bool fast_query_closest(const RtSceneView& S, V3 o, V3 d, STK& stk, float&
 }
 
 // Occlusion query (exact; needs no fallback): is there an M-T-hit triangle
-// whose octree leaf the reference's walk reaches?
+// whose octree leaf the reference's walk reaches? 1 / 0; -1 when the
+// bounded stack overflowed (answer unknown).
 template <class STK>
 RT_HD int fast_query_any(const RtSceneView& S, V3 o, V3 d, STK& stk, Stats* st)
 {
@@ -232,56 +302,57 @@ RT_HD int fast_query_any(const RtSceneView& S, V3 o, V3 d, STK& stk, Stats* st)
     int sp = 0;
     int cur = 0;
     for (;;) {
-        const BvhNodeR n = load_bvh(S.bvh, cur);
-        if (st) st->c[RT_STAT_ANY_VOL] += 2;
-        float tl, tr;
-        const bool hl = n.lcount >= 0 && box_hit(n.lmin, n.lmax, rb, __builtin_inff(), tl);
-        const bool hr = n.rcount >= 0 && box_hit(n.rmin, n.rmax, rb, __builtin_inff(), tr);
-        for (int side = 0; side < 2; side++) {
-            const bool hit = side ? hr : hl;
-            const int cnt = side ? n.rcount : n.lcount;
-            if (!hit || cnt == 0) continue;
-            const int first = side ? n.right : n.left;
+        const Bvh4R n = load_bvh4(S.bvh4, cur);
+        if (st) st->c[RT_STAT_ANY_VOL] += 4;
+        float tn[4];
+        bool hit[4];
+        box4(n, rb, __builtin_inff(), tn, hit);
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+            if (!hit[c] || n.cnt[c] <= 0) continue;
+            const int cnt = n.cnt[c];
             if (st) st->c[RT_STAT_ANY_TRI] += cnt;
-            for (int j = 0; j < cnt; j++) {
+            LeafTris L;
+            load_leaf(S, n.ref[c], cnt, L);
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                if (j >= cnt) break;
                 float t;
-                if (tri_test(S.bvh_tri4, first + j, o, d, t)) {
+                if (tri_test_v(ld3(L.a[j]), ld3(L.e1[j]), ld3(L.e2[j]), o, d, t)) {
                     if (!kset) {
                         ray_setup(o, d, K);
                         kset = true;
                     }
-                    if (chain_ok(S, K, (int)rt_asuint(S.bvh_tri4[3 * (first + j) + 1].w), false, 0.0f, st)) return 1;
+                    if (chain_ok(S, K, (int)rt_asuint(L.e1[j].w), false, 0.0f, st)) return 1;
                 }
             }
         }
-        const bool il = hl && n.lcount == 0, ir = hr && n.rcount == 0;
-        int next = -1;
-        if (il && ir) {
-            const bool lfirst = tl <= tr;
-            next = lfirst ? n.left : n.right;
-            if (sp == STK::CAP) return -1;
-            stk.set_rec(sp++, (uint32_t)(lfirst ? n.right : n.left));
-        } else if (il) {
-            next = n.left;
-        } else if (ir) {
-            next = n.right;
+        cur = -1;
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+            if (!hit[c] || n.cnt[c] != 0) continue;
+            if (cur < 0) {
+                cur = n.ref[c];
+            } else {
+                if (sp == STK::CAP) return -1;
+                stk.set(sp++, (uint32_t)n.ref[c], 0.0f);
+            }
         }
-        if (next >= 0) {
-            cur = next;
-            continue;
-        }
+        if (cur >= 0) continue;
         if (sp == 0) return 0;
         cur = (int)stk.rec(--sp);
     }
 }
 
-// Plain-array node-index stack (host build).
+// Plain-array node stack with keys (host build).
 template <int N>
 struct IdxStack {
     static constexpr int CAP = N;
     uint32_t r[N];
+    float k[N];
     RT_HD uint32_t rec(int i) const { return r[i]; }
-    RT_HD void set_rec(int i, uint32_t v) { r[i] = v; }
+    RT_HD float key(int i) const { return k[i]; }
+    RT_HD void set(int i, uint32_t v, float kv) { r[i] = v, k[i] = kv; }
 };
 
 }  // namespace rtk

@@ -66,7 +66,7 @@ enum {
 
 struct Backend {
     DevBuf nodes, tri4, prim2k, mat_idx, mats, emissive, spheres, env, env_lum, cdf;
-    DevBuf bvh, bvh_tri4, parent, leaf_of, cdf_row, cdf_coarse;
+    DevBuf bvh4, bvh_tri4, parent, leaf_of, cdf_row, cdf_coarse;
     DevBuf stats;     // RT_STAT_COUNT u64
     DevBuf wave;      // path state, pending records, results, queues, lists
     DevBuf counters;  // C_COUNT int32
@@ -227,17 +227,35 @@ __global__ __launch_bounds__(256, 3) void k_step(rtk::WaveView W, int par, unsig
 //    query whose answer needs the exact walk (or whose stack would overflow)
 //    goes to the fallback list for the next launch, and its slot's r_park
 //    count keeps k_step off the path until the walk has finished.
-#define RT_LDS_CAP_FAST 24
-#define RT_LDS_CAP_CLOSEST 8  // key + record: 16 of the 24 words per lane (windows are powers of two)
-#define RT_LDS_CAP_ANY 16
+#define RT_LDS_WORDS 32         // LDS words per lane of k_trace (32 KB per block of 256)
+#define RT_LDS_CAP_FAST 16      // search-BVH stack: node + key in LDS ...
+#define RT_SPILL_FAST RT_FAST_SPILL  // ... then in the lane's global spill area
+#define RT_LDS_CAP_CLOSEST 16   // exact walks: key + record (windows are powers of two)
+#define RT_LDS_CAP_ANY 32
 #define RT_REFILL 16
 
-template <int N>
-struct LdsIdx {
-    static constexpr int CAP = N;
+// Search-BVH stack of a fast query: entries [0, N) in LDS (entry i of
+// thread t at [i * 256 + t]: a wave at equal depth touches 64 consecutive
+// words), the rest in the lane's global spill area (deep stacks are rare).
+template <int N, int M>
+struct FastStack {
+    static constexpr int CAP = N + M;
     uint32_t* r;
-    __device__ __forceinline__ uint32_t rec(int i) const { return r[i * 256]; }
-    __device__ __forceinline__ void set_rec(int i, uint32_t v) { r[i * 256] = v; }
+    float* k;
+    uint32_t* gr;
+    float* gk;
+    __device__ __forceinline__ uint32_t rec(int i) const { return i < N ? r[i * 256] : gr[i - N]; }
+    __device__ __forceinline__ float key(int i) const { return i < N ? k[i * 256] : gk[i - N]; }
+    __device__ __forceinline__ void set(int i, uint32_t rv, float kv)
+    {
+        if (i < N) {
+            r[i * 256] = rv;
+            k[i * 256] = kv;
+        } else {
+            gr[i - N] = rv;
+            gk[i - N] = kv;
+        }
+    }
 };
 
 // Blocks [0, n0) take role 0, the rest role 1, in proportion to the work.
@@ -366,9 +384,9 @@ __device__ void exact_any(const rtk::WaveView& W, int par, uint32_t* lds, int la
 }
 
 template <bool STATS>
-__global__ __launch_bounds__(256, 6) void k_trace(rtk::WaveView W, int par, unsigned long long* stats)
+__global__ __launch_bounds__(256, 4) void k_trace(rtk::WaveView W, int par, unsigned long long* stats)
 {
-    __shared__ uint32_t s_lds[RT_LDS_CAP_FAST * 256];
+    __shared__ uint32_t s_lds[RT_LDS_WORDS * 256];
     int32_t* cnt = W.counters;
     const int32_t* q = cnt + C_Q + par * rtk::RK_COUNT;
     if (blockIdx.x == 0 && threadIdx.x == 0) {  // filled by k_step(i) next
@@ -399,7 +417,9 @@ __global__ __launch_bounds__(256, 6) void k_trace(rtk::WaveView W, int par, unsi
     }
 
     // fast roles
-    LdsIdx<RT_LDS_CAP_FAST> stk{s_lds + threadIdx.x};
+    const size_t gl = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    FastStack<RT_LDS_CAP_FAST, RT_SPILL_FAST> stk{s_lds + threadIdx.x, (float*)s_lds + RT_LDS_CAP_FAST * 256 + threadIdx.x,
+                                                  W.fspill_r + gl * RT_SPILL_FAST, W.fspill_k + gl * RT_SPILL_FAST};
     const int last_kind = W.any_rays ? rtk::RK_BL : rtk::RK_BENV;
     int nc = 0;
     for (int k = rtk::RK_CONT; k <= last_kind; k++) nc += q[k];
@@ -525,7 +545,7 @@ void rt_backend_destroy(rt_context* c)
     if (!b) return;
     (void)hipSetDevice(c->device);
     DevBuf* all[] = {&b->nodes, &b->tri4, &b->prim2k, &b->mat_idx, &b->mats, &b->emissive, &b->spheres, &b->env,
-                     &b->env_lum, &b->cdf, &b->bvh, &b->bvh_tri4, &b->parent, &b->leaf_of, &b->cdf_row, &b->cdf_coarse,
+                     &b->env_lum, &b->cdf, &b->bvh4, &b->bvh_tri4, &b->parent, &b->leaf_of, &b->cdf_row, &b->cdf_coarse,
                      &b->stats, &b->wave,
                      &b->counters, &b->xy, &b->fb};
     for (DevBuf* d : all)
@@ -550,7 +570,7 @@ int rt_backend_upload(rt_context* c)
         (r = upload(c, b->mats, c->mats)) || (r = upload(c, b->emissive, c->emissive)) ||
         (r = upload(c, b->spheres, c->spheres)) || (r = upload(c, b->env, c->env)) ||
         (r = upload(c, b->env_lum, c->env_lum)) || (r = upload(c, b->cdf, c->cdf)) ||
-        (r = upload(c, b->bvh, c->flat.bvh)) || (r = upload(c, b->bvh_tri4, c->flat.bvh_tri4)) ||
+        (r = upload(c, b->bvh4, c->flat.bvh4)) || (r = upload(c, b->bvh_tri4, c->flat.bvh_tri4)) ||
         (r = upload(c, b->parent, c->flat.parent)) || (r = upload(c, b->leaf_of, c->flat.leaf_of)) ||
         (r = upload(c, b->cdf_row, c->cdf_row)) || (r = upload(c, b->cdf_coarse, c->cdf_coarse)) ||
         (r = ensure(c, b->stats, RT_STAT_COUNT * sizeof(unsigned long long))) ||
@@ -576,7 +596,7 @@ int rt_backend_upload(rt_context* c)
     v.eh = c->eh;
     v.n_tris = (int)(c->tris.size() / 9);
     v.chain_monotone = c->flat.chain_monotone ? 1 : 0;
-    v.bvh = (const BvhNode*)b->bvh.p;
+    v.bvh4 = (const Bvh4Node*)b->bvh4.p;
     v.bvh_tri4 = (const float4_*)b->bvh_tri4.p;
     v.parent = (const int32_t*)b->parent.p;
     v.leaf_of = (const int32_t*)b->leaf_of.p;
@@ -595,10 +615,13 @@ static int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounce
     (void)hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, c->device);
     const int threads = 256;
     const int step_blocks = std::min((n + threads - 1) / threads, dev_cus * 8);
-    const int trace_blocks = dev_cus * 8;  // k_trace: wave-strided; 6 blocks (24 KB LDS each) resident per CU
+    // k_trace: wave-strided; 4 blocks resident per CU (128 VGPRs: at 5-6 waves/SIMD the
+    // walk spills to scratch or thrashes the vector L1 and runs slower, measured)
+    const int trace_blocks = dev_cus * 8;
     rtk::WaveView W{};
     W.park_cap = 1 << 16;
     W.spill_lanes = dev_cus * 4 * threads;  // exact walks: up to dev_cus * 2 blocks per role
+    W.fspill_lanes = trace_blocks * threads;
     const size_t need = rtk::wave_carve(nullptr, (size_t)n, W);
     if (int r = ensure(c, b->wave, need)) return r;
     rtk::wave_carve((char*)b->wave.p, (size_t)n, W);

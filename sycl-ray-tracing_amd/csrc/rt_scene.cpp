@@ -644,6 +644,79 @@ struct SahBuilder {
 };
 }  // namespace
 
+// Collapses the binary BVH into a 4-wide one: a node adopts its children,
+// then repeatedly opens its largest-area inner child in favour of that
+// child's two children, while it has fewer than four. Boxes are copied
+// unchanged (still conservatively padded); leaves keep their entries.
+static void collapse_bvh4(const std::vector<BvhNode>& b2, std::vector<Bvh4Node>& b4)
+{
+    struct Slot {
+        float mn[3], mx[3];
+        int32_t ref, cnt;
+        float area() const
+        {
+            const float dx = mx[0] - mn[0], dy = mx[1] - mn[1], dz = mx[2] - mn[2];
+            return dx * dy + dy * dz + dz * dx;
+        }
+    };
+    auto slots_of = [&](int n, Slot* out) {
+        const BvhNode& x = b2[n];
+        for (int i = 0; i < 3; i++) out[0].mn[i] = x.lmin[i], out[0].mx[i] = x.lmax[i];
+        for (int i = 0; i < 3; i++) out[1].mn[i] = x.rmin[i], out[1].mx[i] = x.rmax[i];
+        out[0].ref = x.left, out[0].cnt = x.lcount;
+        out[1].ref = x.right, out[1].cnt = x.rcount;
+    };
+    b4.clear();
+    if (b2.empty()) return;
+    struct Task {
+        int n2, n4;
+    };
+    std::vector<Task> st{{0, 0}};
+    b4.emplace_back();
+    while (!st.empty()) {
+        const Task t = st.back();
+        st.pop_back();
+        Slot c[4];
+        int m = 2;
+        slots_of(t.n2, c);
+        while (m < 4) {
+            int best = -1;
+            for (int i = 0; i < m; i++)
+                if (c[i].cnt == 0 && (best < 0 || c[i].area() > c[best].area())) best = i;
+            if (best < 0) break;
+            Slot two[2];
+            slots_of(c[best].ref, two);
+            c[best] = two[0];
+            c[m++] = two[1];
+        }
+        Bvh4Node nd{};
+        for (int i = 0; i < 4; i++) {
+            if (i >= m || c[i].cnt < 0) {
+                nd.lox[i] = nd.loy[i] = nd.loz[i] = INFINITY;
+                nd.hix[i] = nd.hiy[i] = nd.hiz[i] = -INFINITY;
+                nd.ref[i] = 0;
+                nd.cnt[i] = -1;
+                continue;
+            }
+            nd.lox[i] = c[i].mn[0], nd.loy[i] = c[i].mn[1], nd.loz[i] = c[i].mn[2];
+            nd.hix[i] = c[i].mx[0], nd.hiy[i] = c[i].mx[1], nd.hiz[i] = c[i].mx[2];
+            nd.cnt[i] = c[i].cnt;
+            nd.ref[i] = c[i].ref;
+        }
+        // inner children get consecutive slots; their subtrees follow depth-first
+        Task kids[4];
+        int nk = 0;
+        for (int i = 0; i < 4; i++)
+            if (nd.cnt[i] == 0) {
+                kids[nk++] = {nd.ref[i], (int)b4.size()};
+                nd.ref[i] = (int)b4.size();
+                b4.emplace_back();
+            }
+        b4[t.n4] = nd;
+        for (int i = nk - 1; i >= 0; i--) st.push_back(kids[i]);
+    }
+}
+
 void build_search_bvh(FlatBvh& out)
 {
     // plane nesting along every parent link (enables rt_fast.h's one-test chain check)
@@ -687,6 +760,7 @@ void build_search_bvh(FlatBvh& out)
         r.lcount = r.rcount = -1;
         out.bvh.push_back(r);
     }
+    collapse_bvh4(out.bvh, out.bvh4);
 }
 
 // ======================================================================= env

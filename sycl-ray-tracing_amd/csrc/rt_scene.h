@@ -61,7 +61,8 @@ struct FlatBvh {
     int max_depth = 0;            // deepest non-empty node
     bool chain_monotone = false;  // every record's planes lie within its parent's
     // search BVH over tri4 (build_search_bvh)
-    std::vector<BvhNode> bvh;
+    std::vector<BvhNode> bvh;    // binary SAH build
+    std::vector<Bvh4Node> bvh4;  // collapsed 4-wide form the device walks
     std::vector<float4_> bvh_tri4;
 };
 void flatten_octree(const Octree& t, const float* tris, int ntris, FlatBvh& out);

@@ -192,9 +192,8 @@ RT_HD bool slab_test(const RtNode& nd, const RayK& k, float& tnear)
 }
 
 // Triangle::intersect (triangle.h:16-60) on the pre-subtracted record.
-RT_HD bool tri_test(const float4_* tri4, int k, V3 o, V3 d, float& t_out)
+RT_HD bool tri_test_v(V3 a, V3 e1, V3 e2, V3 o, V3 d, float& t_out)
 {
-    const V3 a = ld3(tri4[3 * k]), e1 = ld3(tri4[3 * k + 1]), e2 = ld3(tri4[3 * k + 2]);
     const float EPS = 0.0000001f;
     V3 h = cross(d, e2);
     float det = dot(e1, h);
@@ -212,6 +211,10 @@ RT_HD bool tri_test(const float4_* tri4, int k, V3 o, V3 d, float& t_out)
         return true;
     }
     return false;
+}
+RT_HD bool tri_test(const float4_* tri4, int k, V3 o, V3 d, float& t_out)
+{
+    return tri_test_v(ld3(tri4[3 * k]), ld3(tri4[3 * k + 1]), ld3(tri4[3 * k + 2]), o, d, t_out);
 }
 
 // ------------------------------------------------ libstdc++ heap emulation

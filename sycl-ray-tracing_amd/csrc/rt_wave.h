@@ -107,6 +107,9 @@ struct WaveView {
     uint32_t* spill_r;      // per-lane stack spill areas of the trace kernels
     float* spill_k;
     int spill_lanes;
+    uint32_t* fspill_r;     // per-lane spill areas of the search-BVH stacks (RT_FAST_SPILL entries)
+    float* fspill_k;
+    int fspill_lanes;
     const int32_t* act_in;  // active slots this iteration
     int32_t* act_out;
     int n_act_in;
@@ -114,7 +117,9 @@ struct WaveView {
 
 // Carves the path-slot buffers for n slots out of one allocation at `base`
 // (nullptr: only sizes it). Returns the bytes needed.
-inline size_t wave_carve(char* base, size_t n, WaveView& W)  // uses W.park_cap, W.spill_lanes
+#define RT_FAST_SPILL 48  // search-BVH stack entries per lane beyond the LDS window
+
+inline size_t wave_carve(char* base, size_t n, WaveView& W)  // uses W.park_cap, W.spill_lanes, W.fspill_lanes
 {
     size_t o = 0;
     auto take = [&](size_t bytes) -> void* {
@@ -155,6 +160,8 @@ inline size_t wave_carve(char* base, size_t n, WaveView& W)  // uses W.park_cap,
     }
     W.spill_r = (uint32_t*)take((size_t)W.spill_lanes * RT_STACK_CAP * 4);
     W.spill_k = (float*)take((size_t)W.spill_lanes * RT_STACK_CAP * 4);
+    W.fspill_r = (uint32_t*)take((size_t)W.fspill_lanes * RT_FAST_SPILL * 4);
+    W.fspill_k = (float*)take((size_t)W.fspill_lanes * RT_FAST_SPILL * 4);
     return o;
 }
 
