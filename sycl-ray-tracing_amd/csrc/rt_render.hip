@@ -19,6 +19,9 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <string>
+#include <vector>
+#include <algorithm>
 
 #include "rt_context.h"
 #include "rt_wave.h"
@@ -439,6 +442,13 @@ __global__ __launch_bounds__(256, 4) void k_trace(rtk::WaveView W, int par, unsi
         bool fail = false;
         rtk::RayRec r;
         uint32_t target = 0;
+#ifdef RT_CHUNK_TRACE
+        // debug build: per-chunk wall time and per-lane work (tools/chunk_trace.py)
+        rtk::Stats qs;
+        for (int i = 0; i < RT_STAT_COUNT; i++) qs.c[i] = 0;
+        ps = &qs;
+        const uint64_t t_chunk = __builtin_amdgcn_s_memrealtime();
+#endif
         if (idx < total) {
             if (closest) {
                 r = rtk::queue_item(W, q, rtk::RK_CONT, last_kind, idx, target);
@@ -457,6 +467,35 @@ __global__ __launch_bounds__(256, 4) void k_trace(rtk::WaveView W, int par, unsi
                     fail = true;
             }
         }
+#ifdef RT_CHUNK_TRACE
+        if (W.ctrace) {
+            const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
+            int vis = (int)((qs.c[RT_STAT_VOL] + qs.c[RT_STAT_ANY_VOL]) / 4);  // 4 box tests per node
+            int tri = (int)(qs.c[RT_STAT_TRI] + qs.c[RT_STAT_ANY_TRI]);
+            int vmax = vis, vsum = vis, tsum = tri;
+            for (int o = 32; o > 0; o >>= 1) {
+                vmax = max(vmax, __shfl_xor(vmax, o));
+                vsum += __shfl_xor(vsum, o);
+                tsum += __shfl_xor(tsum, o);
+            }
+            if (lane_id() == 0) {
+                const int rec = atomicAdd(W.ctrace_n, 1);
+                if (rec < W.ctrace_cap) {
+                    uint32_t* o = W.ctrace + 8 * (size_t)rec;
+                    unsigned xcc;
+                    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+                    o[0] = (uint32_t)(t_chunk - W.ctrace_t0);
+                    o[1] = (uint32_t)(t_end - W.ctrace_t0);
+                    o[2] = (uint32_t)vmax;
+                    o[3] = (uint32_t)vsum;
+                    o[4] = (uint32_t)tsum;
+                    o[5] = (uint32_t)(closest ? 1 : 2) | ((xcc & 15u) << 4);
+                    o[6] = (uint32_t)(blockIdx.x * 4 + (threadIdx.x >> 6));
+                    o[7] = (uint32_t)min(64, total - base);
+                }
+            }
+        }
+#endif
         const int f = wave_append(fbn, fail);
         if (fail) {
             r.d.w = rt_asfloat(target & 7u);
@@ -672,10 +711,47 @@ static int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounce
         W.act_in = lists[par];
         W.act_out = lists[par ^ 1];
         if (T) HIPCHK(c, hipEventRecord(b->tev[0][it], s));
+#ifdef RT_CHUNK_TRACE
+        // debug build: record every chunk of the k_trace launches of the
+        // iterations listed in RT_CHUNK_TRACE_ITERS into RT_CHUNK_TRACE_OUT.<it>
+        bool ct = false;
+        if (const char* e = getenv("RT_CHUNK_TRACE_ITERS")) {
+            char key[32];
+            snprintf(key, sizeof key, ",%d,", it);
+            ct = strstr((std::string(",") + e + ",").c_str(), key) != nullptr;
+        }
+        static uint32_t* d_ct = nullptr;
+        const int ct_cap = 1 << 18;
+        if (ct) {
+            if (!d_ct) HIPCHK(c, hipMalloc(&d_ct, (size_t)ct_cap * 32 + 256));
+            HIPCHK(c, hipMemsetAsync(d_ct, 0, 256, s));
+            W.ctrace_n = (int32_t*)d_ct;
+            W.ctrace = d_ct + 64;
+            W.ctrace_cap = ct_cap;
+            W.ctrace_t0 = 0;
+        }
+#endif
         if (S)
             hipLaunchKernelGGL(k_trace<true>, dim3(trace_blocks), dim3(threads), 0, s, W, par, stats);
         else
             hipLaunchKernelGGL(k_trace<false>, dim3(trace_blocks), dim3(threads), 0, s, W, par, stats);
+#ifdef RT_CHUNK_TRACE
+        if (ct) {
+            HIPCHK(c, hipStreamSynchronize(s));
+            int32_t nrec = 0;
+            HIPCHK(c, hipMemcpy(&nrec, d_ct, 4, hipMemcpyDeviceToHost));
+            nrec = std::min(nrec, ct_cap);
+            std::vector<uint32_t> h((size_t)nrec * 8);
+            HIPCHK(c, hipMemcpy(h.data(), d_ct + 64, h.size() * 4, hipMemcpyDeviceToHost));
+            const char* outp = getenv("RT_CHUNK_TRACE_OUT");
+            std::string path = std::string(outp ? outp : "chunk_trace") + "." + std::to_string(it);
+            if (FILE* f = fopen(path.c_str(), "wb")) {
+                fwrite(h.data(), 4, h.size(), f);
+                fclose(f);
+            }
+            W.ctrace = nullptr;
+        }
+#endif
         if (T) HIPCHK(c, hipEventRecord(b->tev[1][it], s));
         if (S)
             hipLaunchKernelGGL(k_step<true>, dim3(step_blocks), dim3(threads), 0, s, W, par, stats);

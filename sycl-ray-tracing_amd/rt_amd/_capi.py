@@ -13,7 +13,7 @@ import os
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_DIR = os.path.join(PKG_DIR, "lib")
-PRODUCT = os.path.join(LIB_DIR, "librt_hip.so")
+PRODUCT = os.environ.get("RT_HIP_LIB") or os.path.join(LIB_DIR, "librt_hip.so")  # (override: debug builds)
 HOSTSIM = os.path.join(LIB_DIR, "librt_hostsim.so")
 
 # every symbol declared in include/rt_hip.h (tests check the export table)
