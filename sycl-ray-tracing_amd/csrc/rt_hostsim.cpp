@@ -54,6 +54,8 @@ static int run_wave_host(rt_context* c, int w, int h, int spp, int bounces, cons
     rtk::WaveView W{};
     W.park_cap = 1 << 14;
     W.spill_lanes = 0;  // the host threads keep their own spill areas
+    W.shards = 1;       // one segment per queue (plain atomics on the host)
+    W.seg_cap = n;
     std::vector<char> arena(rtk::wave_carve(nullptr, (size_t)n, W));
     rtk::wave_carve(arena.data(), (size_t)n, W);
     W.S = rt_host_view(c);

@@ -50,9 +50,14 @@ struct DevBuf {
 //   FB[p]     fallback sizes  filled by k_trace(i-1), read by k_trace(i), which fills FB[p^1]; k_step(i) zeroes FB[p]
 //   PARK[p]   parked queries  likewise
 //   TK        exact-walk work tickets of k_trace(i); k_step(i) zeroes them
+//
+// Q and ACT are sharded: the appends of a 64-item input chunk c go to
+// shard c % RT_QSHARDS, each shard a segment of W.seg_cap entries with its
+// own counter on its own 128-B line. One counter per queue took every
+// wave's atomic: ~630 us per 2 M appends on 6 counters against ~25 us
+// sharded 64 ways (tools/micro/atomics.hip on the MI355X).
 enum {
-    C_Q = 0,  // + set * RK_COUNT + kind
-    C_FBC0 = 2 * rtk::RK_COUNT,
+    C_FBC0 = 0,
     C_FBC1,
     C_FBA0,
     C_FBA1,
@@ -62,10 +67,19 @@ enum {
     C_PARKA1,
     C_TK_EXACT_C,
     C_TK_EXACT_A,
-    C_ACT0,
-    C_ACT1,
-    C_COUNT
+    C_SHARDED = 64,  // sharded counters from here (qc_at / ac_at)
 };
+#define RT_QSHARDS 64
+#define RT_CSTRIDE 32  // ints from one sharded counter to the next (one 128-B line each)
+#define C_COUNT (C_SHARDED + (2 * rtk::RK_COUNT + 2) * RT_QSHARDS * RT_CSTRIDE)
+__host__ __device__ __forceinline__ int qc_at(int par, int kind, int shard)
+{
+    return C_SHARDED + ((par * rtk::RK_COUNT + kind) * RT_QSHARDS + shard) * RT_CSTRIDE;
+}
+__host__ __device__ __forceinline__ int ac_at(int par, int shard)
+{
+    return C_SHARDED + ((2 * rtk::RK_COUNT + par) * RT_QSHARDS + shard) * RT_CSTRIDE;
+}
 
 struct Backend {
     DevBuf nodes, tri4, prim2k, mat_idx, mats, emissive, spheres, env, env_lum, cdf;
@@ -75,7 +89,7 @@ struct Backend {
     DevBuf counters;  // C_COUNT int32
     DevBuf xy;        // pixel list (rt_render_pixels)
     DevBuf fb;        // host-fb staging
-    int32_t* h_act = nullptr;  // pinned host copy of a live-slot count
+    int32_t* h_act = nullptr;  // pinned host copy of the live-slot counters (sharded)
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     RtSceneView view{};
     int bl_rays = 1, any_rays = 1;
@@ -161,17 +175,59 @@ __device__ __forceinline__ void flush_stats(const rtk::Stats& st, unsigned long 
 }
 
 // ------------------------------------------------------------------ kernels
-__device__ __forceinline__ void append_emit(const rtk::WaveView& W, int32_t* qcount, int32_t* act_count, int p,
-                                            const rtk::Emit& e)
+// Appends what the wave's lanes emitted to the queues and the live list of
+// parity pout, in the shard of the 64-item input chunk `base` (whole wave).
+__device__ __forceinline__ void append_emit(const rtk::WaveView& W, int pout, int base, int p, const rtk::Emit& e)
 {
+    const int sh = (base >> 6) % RT_QSHARDS;
+    const size_t seg = (size_t)sh * W.seg_cap;
 #pragma unroll
     for (int k = 0; k < rtk::RK_COUNT; k++) {
         const bool want = (e.mask >> k) & 1u;
-        const int i = wave_append(qcount + k, want);
-        if (want) W.q[k][i] = e.r[k];
+        const int i = wave_append(W.counters + qc_at(pout, k, sh), want);
+        if (want) W.q[k][seg + i] = e.r[k];
     }
-    const int a = wave_append(act_count, e.active);
-    if (e.active) W.act_out[a] = p;
+    const int a = wave_append(W.counters + ac_at(pout, sh), e.active);
+    if (e.active) W.act_out[seg + a] = p;
+}
+
+// Exclusive prefix sums of the sharded counters at cnt[at(j)], j < m (m a
+// multiple of 64), into pre[0..m] (LDS); every thread of the block calls.
+template <class AT>
+__device__ __forceinline__ void shard_prefix(const int32_t* cnt, int m, AT at, int* pre)
+{
+    const int nw = (int)(blockDim.x >> 6), w = (int)(threadIdx.x >> 6);
+    for (int g = w; g < m / 64; g += nw) {  // one wave per 64 counters: inclusive scan
+        int v = cnt[at(g * 64 + lane_id())];
+        for (int o = 1; o < 64; o <<= 1) {
+            const int u = __shfl_up(v, o);
+            if (lane_id() >= o) v += u;
+        }
+        pre[g * 64 + lane_id() + 1] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {  // chain the groups
+        pre[0] = 0;
+        for (int g = 1; g < m / 64; g++) {
+            const int off = pre[g * 64];
+            for (int j = 1; j <= 64; j++) pre[g * 64 + j] += off;
+        }
+    }
+    __syncthreads();
+}
+
+// Segment j of a prefix table pre[0..m] holding global index g (pre[j] <= g < pre[j+1]).
+__device__ __forceinline__ int shard_find(const int* pre, int m, int g)
+{
+    int lo = 0, hi = m - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (pre[mid] <= g)
+            lo = mid;
+        else
+            hi = mid - 1;
+    }
+    return lo;
 }
 
 // Path init: every slot seeds its RNG and emits its first camera ray (into Q[0], ACT[0]).
@@ -182,20 +238,20 @@ __global__ __launch_bounds__(256) void k_init(rtk::WaveView W)
     e.mask = 0;
     e.active = false;
     if (p < W.n_slots) rtk::path_init(W, p, e);
-    append_emit(W, W.counters + C_Q, W.counters + C_ACT0, p, e);
+    append_emit(W, 0, p & ~63, p, e);
 }
 
 template <bool STATS>
 __global__ __launch_bounds__(256, 3) void k_step(rtk::WaveView W, int par, unsigned long long* stats)
 {
+    __shared__ int s_pre[RT_QSHARDS + 1];
     int32_t* cnt = W.counters;
     if (blockIdx.x == 0 && threadIdx.x == 0) {  // read by k_trace(i); refilled by k_trace(i + 1)
         cnt[C_FBC0 + par] = cnt[C_FBA0 + par] = cnt[C_PARKC0 + par] = cnt[C_PARKA0 + par] = 0;
         cnt[C_TK_EXACT_C] = cnt[C_TK_EXACT_A] = 0;
     }
-    const int n = cnt[C_ACT0 + par];
-    int32_t* qout = cnt + C_Q + (par ^ 1) * rtk::RK_COUNT;
-    int32_t* aout = cnt + C_ACT0 + (par ^ 1);
+    shard_prefix(cnt, RT_QSHARDS, [&](int j) { return ac_at(par, j); }, s_pre);
+    const int n = s_pre[RT_QSHARDS];
     rtk::Stats st;
     if (STATS)
         for (int i = 0; i < RT_STAT_COUNT; i++) st.c[i] = 0;
@@ -206,10 +262,11 @@ __global__ __launch_bounds__(256, 3) void k_step(rtk::WaveView W, int par, unsig
         e.active = false;
         int p = -1;
         if (idx < n) {
-            p = W.act_in[idx];
+            const int sh = shard_find(s_pre, RT_QSHARDS, idx);
+            p = W.act_in[(size_t)sh * W.seg_cap + (idx - s_pre[sh])];
             rtk::path_step(W, p, e, STATS ? &st : nullptr);
         }
-        append_emit(W, qout, aout, p, e);
+        append_emit(W, par ^ 1, base, p, e);
     }
     flush_stats<STATS>(st, stats);
 }
@@ -390,12 +447,12 @@ template <bool STATS>
 __global__ __launch_bounds__(256, 4) void k_trace(rtk::WaveView W, int par, unsigned long long* stats)
 {
     __shared__ uint32_t s_lds[RT_LDS_WORDS * 256];
+    __shared__ int s_pre[rtk::RK_COUNT * RT_QSHARDS + 1];
     int32_t* cnt = W.counters;
-    const int32_t* q = cnt + C_Q + par * rtk::RK_COUNT;
-    if (blockIdx.x == 0 && threadIdx.x == 0) {  // filled by k_step(i) next
-        for (int k = 0; k < rtk::RK_COUNT; k++) cnt[C_Q + (par ^ 1) * rtk::RK_COUNT + k] = 0;
-        cnt[C_ACT0 + (par ^ 1)] = 0;
-    }
+    if (blockIdx.x == 0)  // filled by k_step(i) next
+        for (int j = threadIdx.x; j < (rtk::RK_COUNT + 1) * RT_QSHARDS; j += blockDim.x)
+            cnt[j < rtk::RK_COUNT * RT_QSHARDS ? qc_at(par ^ 1, j / RT_QSHARDS, j % RT_QSHARDS)
+                                                : ac_at(par ^ 1, j - rtk::RK_COUNT * RT_QSHARDS)] = 0;
     rtk::Stats st;
     if (STATS)
         for (int i = 0; i < RT_STAT_COUNT; i++) st.c[i] = 0;
@@ -423,10 +480,13 @@ __global__ __launch_bounds__(256, 4) void k_trace(rtk::WaveView W, int par, unsi
     const size_t gl = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     FastStack<RT_LDS_CAP_FAST, RT_SPILL_FAST> stk{s_lds + threadIdx.x, (float*)s_lds + RT_LDS_CAP_FAST * 256 + threadIdx.x,
                                                   W.fspill_r + gl * RT_SPILL_FAST, W.fspill_k + gl * RT_SPILL_FAST};
+    // queue segments (kind-major, then shard): prefix table in LDS
+    shard_prefix(cnt, rtk::RK_COUNT * RT_QSHARDS,
+                 [&](int j) { return qc_at(par, j / RT_QSHARDS, j % RT_QSHARDS); }, s_pre);
     const int last_kind = W.any_rays ? rtk::RK_BL : rtk::RK_BENV;
-    int nc = 0;
-    for (int k = rtk::RK_CONT; k <= last_kind; k++) nc += q[k];
-    const int na = W.any_rays ? q[rtk::RK_ESH] + q[rtk::RK_BENV] : 0;
+    const int c0 = s_pre[rtk::RK_CONT * RT_QSHARDS], a0 = s_pre[rtk::RK_ESH * RT_QSHARDS];
+    const int nc = s_pre[(last_kind + 1) * RT_QSHARDS] - c0;
+    const int na = W.any_rays ? s_pre[(rtk::RK_BENV + 1) * RT_QSHARDS] - a0 : 0;
     const int fb0 = nbe_c + nbe_a, nbf = (int)gridDim.x - fb0;
     const int nbc = split_blocks(nbf, nc, na);
     const bool closest = b - fb0 < nbc;
@@ -450,8 +510,13 @@ __global__ __launch_bounds__(256, 4) void k_trace(rtk::WaveView W, int par, unsi
         const uint64_t t_chunk = __builtin_amdgcn_s_memrealtime();
 #endif
         if (idx < total) {
+            // queue item: segment (kind, shard) of global index g
+            const int g = (closest ? c0 : a0) + idx;
+            const int seg = shard_find(s_pre, rtk::RK_COUNT * RT_QSHARDS, g);
+            const int kind = seg / RT_QSHARDS;
+            r = W.q[kind][(size_t)(seg % RT_QSHARDS) * W.seg_cap + (g - s_pre[seg])];
+            target = (rt_asuint(r.o.w) << 3) | (uint32_t)kind;
             if (closest) {
-                r = rtk::queue_item(W, q, rtk::RK_CONT, last_kind, idx, target);
                 float t;
                 int k;
                 if (rtk::fast_query_closest(W.S, rtk::v3of(r.o), rtk::v3of(r.d), stk, t, k, ps))
@@ -459,7 +524,6 @@ __global__ __launch_bounds__(256, 4) void k_trace(rtk::WaveView W, int par, unsi
                 else
                     fail = true;
             } else {
-                r = rtk::queue_item(W, q, rtk::RK_ESH, rtk::RK_BENV, idx, target);
                 const int a = rtk::fast_query_any(W.S, rtk::v3of(r.o), rtk::v3of(r.d), stk, ps);
                 if (a >= 0)
                     rtk::finish_any(W, target, a == 1);
@@ -573,7 +637,7 @@ int rt_backend_create(rt_context* c)
     c->backend = b;
     HIPCHK(c, hipEventCreate(&b->ev0));
     HIPCHK(c, hipEventCreate(&b->ev1));
-    HIPCHK(c, hipHostMalloc((void**)&b->h_act, 16, hipHostMallocDefault));
+    HIPCHK(c, hipHostMalloc((void**)&b->h_act, RT_QSHARDS * RT_CSTRIDE * 4, hipHostMallocDefault));
     if (const char* e = getenv("RT_STEP_BUDGET")) b->budget = std::max(1, atoi(e));
     return RT_OK;
 }
@@ -659,6 +723,8 @@ static int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounce
     const int trace_blocks = dev_cus * 8;
     rtk::WaveView W{};
     W.park_cap = 1 << 16;
+    W.shards = RT_QSHARDS;
+    W.seg_cap = 64 * (((n + 63) / 64 + RT_QSHARDS - 1) / RT_QSHARDS);  // 64-item chunk c -> shard c % RT_QSHARDS
     W.spill_lanes = dev_cus * 4 * threads;  // exact walks: up to dev_cus * 2 blocks per role
     W.fspill_lanes = trace_blocks * threads;
     const size_t need = rtk::wave_carve(nullptr, (size_t)n, W);
@@ -694,7 +760,7 @@ static int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounce
     HIPCHK(c, hipGetLastError());
 
     // Two launches per iteration (k_trace, k_step); the counter sets they
-    // fill are double-buffered by iteration parity (see C_Q).
+    // fill are double-buffered by iteration parity (see C_FBC0).
     // A sample takes at most bounces + 1 iterations without fallbacks; an
     // exact walk delays its path by at least one iteration. The bound only
     // guards against a runaway loop.
@@ -760,9 +826,12 @@ static int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounce
         if (T) HIPCHK(c, hipEventRecord(b->tev[2][it], s));
         HIPCHK(c, hipGetLastError());
         if ((it & 7) == 7) {
-            HIPCHK(c, hipMemcpyAsync(b->h_act, cnt + C_ACT0 + (par ^ 1), 4, hipMemcpyDeviceToHost, s));
+            HIPCHK(c, hipMemcpyAsync(b->h_act, cnt + ac_at(par ^ 1, 0), RT_QSHARDS * RT_CSTRIDE * 4,
+                                     hipMemcpyDeviceToHost, s));
             HIPCHK(c, hipStreamSynchronize(s));
-            done = *b->h_act == 0;
+            long live = 0;
+            for (int j = 0; j < RT_QSHARDS; j++) live += b->h_act[j * RT_CSTRIDE];
+            done = live == 0;
         }
     }
     if (!done) {

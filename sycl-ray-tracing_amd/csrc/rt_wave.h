@@ -114,6 +114,7 @@ struct WaveView {
     int32_t* ctrace_n;
     int ctrace_cap;
     uint64_t ctrace_t0;
+    int shards, seg_cap;    // queues and live lists: `shards` segments of seg_cap entries (device: rt_render.hip)
     const int32_t* act_in;  // active slots this iteration
     int32_t* act_out;
     int n_act_in;
@@ -123,7 +124,7 @@ struct WaveView {
 // (nullptr: only sizes it). Returns the bytes needed.
 #define RT_FAST_SPILL 48  // search-BVH stack entries per lane beyond the LDS window
 
-inline size_t wave_carve(char* base, size_t n, WaveView& W)  // uses W.park_cap, W.spill_lanes, W.fspill_lanes
+inline size_t wave_carve(char* base, size_t n, WaveView& W)  // uses W.park_cap, W.spill_lanes, W.fspill_lanes, W.shards, W.seg_cap
 {
     size_t o = 0;
     auto take = [&](size_t bytes) -> void* {
@@ -152,9 +153,10 @@ inline size_t wave_carve(char* base, size_t n, WaveView& W)  // uses W.park_cap,
     W.r_bl_k = (int32_t*)take(n * 4);
     W.r_esh = (uint8_t*)take(n);
     W.r_benv = (uint8_t*)take(n);
-    for (int k = 0; k < RK_COUNT; k++) W.q[k] = (RayRec*)take(n * sizeof(RayRec));
-    W.act_in = (const int32_t*)take(n * 4);
-    W.act_out = (int32_t*)take(n * 4);
+    const size_t qn = (size_t)W.shards * W.seg_cap;  // >= n
+    for (int k = 0; k < RK_COUNT; k++) W.q[k] = (RayRec*)take(qn * sizeof(RayRec));
+    W.act_in = (const int32_t*)take(qn * 4);
+    W.act_out = (int32_t*)take(qn * 4);
     W.r_park = (int32_t*)take(n * 4);
     for (int k = 0; k < 2; k++) {
         W.fb_c[k] = (RayRec*)take(5 * n * sizeof(RayRec));
