@@ -51,9 +51,9 @@ struct DevBuf {
 //   PARK[p]   parked queries  likewise
 //   TK        exact-walk work tickets of k_trace(i); k_step(i) zeroes them
 //
-// Q and ACT are sharded: the appends of a 64-item input chunk c go to
-// shard c % RT_QSHARDS, each shard a segment of W.seg_cap entries with its
-// own counter on its own 128-B line. One counter per queue took every
+// Q and ACT are sharded: the appends of a 64-item input chunk go to one of
+// RT_QSHARDS shards (append_emit), each a segment of W.seg_cap entries with
+// its own counter on its own 128-B line. One counter per queue took every
 // wave's atomic: ~630 us per 2 M appends on 6 counters against ~25 us
 // sharded 64 ways (tools/micro/atomics.hip on the MI355X).
 enum {
@@ -177,9 +177,13 @@ __device__ __forceinline__ void flush_stats(const rtk::Stats& st, unsigned long 
 // ------------------------------------------------------------------ kernels
 // Appends what the wave's lanes emitted to the queues and the live list of
 // parity pout, in the shard of the 64-item input chunk `base` (whole wave).
-__device__ __forceinline__ void append_emit(const rtk::WaveView& W, int pout, int base, int p, const rtk::Emit& e)
+// Shards take contiguous runs of the n_in inputs' chunks, so a queue read in
+// order follows its input order (pixel order, through the compactions).
+__device__ __forceinline__ void append_emit(const rtk::WaveView& W, int pout, int base, int n_in, int p,
+                                            const rtk::Emit& e)
 {
-    const int sh = (base >> 6) % RT_QSHARDS;
+    const int cps = ((n_in + 63) / 64 + RT_QSHARDS - 1) / RT_QSHARDS;  // chunks per shard
+    const int sh = min(RT_QSHARDS - 1, (base >> 6) / cps);
     const size_t seg = (size_t)sh * W.seg_cap;
 #pragma unroll
     for (int k = 0; k < rtk::RK_COUNT; k++) {
@@ -238,7 +242,7 @@ __global__ __launch_bounds__(256) void k_init(rtk::WaveView W)
     e.mask = 0;
     e.active = false;
     if (p < W.n_slots) rtk::path_init(W, p, e);
-    append_emit(W, 0, p & ~63, p, e);
+    append_emit(W, 0, p & ~63, W.n_slots, p, e);
 }
 
 template <bool STATS>
@@ -266,7 +270,7 @@ __global__ __launch_bounds__(256, 3) void k_step(rtk::WaveView W, int par, unsig
             p = W.act_in[(size_t)sh * W.seg_cap + (idx - s_pre[sh])];
             rtk::path_step(W, p, e, STATS ? &st : nullptr);
         }
-        append_emit(W, par ^ 1, base, p, e);
+        append_emit(W, par ^ 1, base, n, p, e);
     }
     flush_stats<STATS>(st, stats);
 }
@@ -724,7 +728,7 @@ static int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounce
     rtk::WaveView W{};
     W.park_cap = 1 << 16;
     W.shards = RT_QSHARDS;
-    W.seg_cap = 64 * (((n + 63) / 64 + RT_QSHARDS - 1) / RT_QSHARDS);  // 64-item chunk c -> shard c % RT_QSHARDS
+    W.seg_cap = 64 * (((n + 63) / 64 + RT_QSHARDS - 1) / RT_QSHARDS);  // (append_emit: chunks per shard)
     W.spill_lanes = dev_cus * 4 * threads;  // exact walks: up to dev_cus * 2 blocks per role
     W.fspill_lanes = trace_blocks * threads;
     const size_t need = rtk::wave_carve(nullptr, (size_t)n, W);
