@@ -119,6 +119,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-stats", action="store_true", help="skip the counter pass (roofline.achieved = null)")
     ap.add_argument("--cpu-row-step", type=int, default=10)
+    ap.add_argument("--sim-world", type=int, default=0,
+                    help="diagnostic: render only rank 0's rows of an N-GPU run, on this one GPU (not a bench line)")
     args = ap.parse_args()
 
     import torch
@@ -148,7 +150,7 @@ def main():
                              P.emissive_triangle_indices, P.material_indices, None, rt_amd.BVH(P.triangles),
                              rt_amd.Image.from_rgb(sky), None, device=local)
     rk.set_camera(rt_amd.Camera(cam17[:16], cam17[16]))
-    frame = ShardedFrame(rk, rank, world, device=dev)
+    frame = ShardedFrame(rk, rank, args.sim_world or world, device=dev)
     info = rk.bvh_info()
     log(f"[rank {rank}] setup {time.time() - t0:.1f}s  bvh {info}")
 
@@ -166,7 +168,8 @@ def main():
 
     for _ in range(args.warmup):
         frame.render(stream)
-        frame.gather()
+        if not args.sim_world:
+            frame.gather()
     torch.cuda.synchronize(dev)
 
     if world > 1:
@@ -177,7 +180,7 @@ def main():
     t_start = time.perf_counter()
     for _ in range(args.steps):
         frame.render(stream)
-        full = frame.gather()
+        full = frame.gather() if not args.sim_world else frame.shard
         kms.append(rk.device_last_kernel_ms())
     torch.cuda.synchronize(dev)
     if world > 1:
@@ -192,7 +195,7 @@ def main():
     elapsed = float(t.item())
     kernel_ms = float(np.mean(kms))
 
-    samples_per_step = W * H * spp
+    samples_per_step = W * H * spp if not args.sim_world else frame.rows * W * spp
     value = samples_per_step * args.steps / elapsed / 1e6
 
     roofline = None

@@ -47,9 +47,16 @@ static_assert(sizeof(BvhNode) == 64, "BvhNode must be 64 B");
 // node is 8 float4 loads and four slab tests in lock-step. Child c: inner
 // node index (cnt 0), leaf's first entry in bvh_tri4 (cnt 1..4) or nothing
 // (cnt -1, box empty).
+// Search-BVH node: four 32-B child records {lo.xyz, hi.xyz, ref, cnt}, so one
+// lane can load one child with two 16-B loads (rt_fast.h quad walks).
+// cnt: -1 empty slot, 0 inner node (ref = node index), > 0 leaf of cnt
+// triangles starting at bvh_tri4 record 3 * ref.
+struct Bvh4Child {
+    float lo[3], hi[3];
+    int32_t ref, cnt;
+};
 struct alignas(128) Bvh4Node {
-    float lox[4], hix[4], loy[4], hiy[4], loz[4], hiz[4];
-    int32_t ref[4], cnt[4];
+    Bvh4Child ch[4];
 };
 static_assert(sizeof(Bvh4Node) == 128, "Bvh4Node must be 128 B");
 

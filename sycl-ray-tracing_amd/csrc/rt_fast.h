@@ -67,24 +67,27 @@ struct Bvh4R {
     float lo[3][4], hi[3][4];
     int32_t ref[4], cnt[4];
 };
+// Child c of a node is records 2c ({lo.xyz, hi.x}) and 2c + 1 ({hi.yz, ref, cnt}).
+RT_HD Bvh4R bvh4_unpack(const float4_* q)
+{
+    Bvh4R n;
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+        const float4_ a = q[2 * c], b = q[2 * c + 1];
+        n.lo[0][c] = a.x, n.lo[1][c] = a.y, n.lo[2][c] = a.z;
+        n.hi[0][c] = a.w, n.hi[1][c] = b.x, n.hi[2][c] = b.y;
+        n.ref[c] = (int32_t)rt_asuint(b.z);
+        n.cnt[c] = (int32_t)rt_asuint(b.w);
+    }
+    return n;
+}
 RT_HD Bvh4R load_bvh4(const Bvh4Node* nodes, int i)
 {
     const float4_* p = (const float4_*)(nodes + i);
     float4_ q[8];
 #pragma unroll
     for (int j = 0; j < 8; j++) q[j] = p[j];
-    Bvh4R n;
-#pragma unroll
-    for (int ax = 0; ax < 3; ax++) {
-        const float4_ l = q[2 * ax], h = q[2 * ax + 1];
-        n.lo[ax][0] = l.x, n.lo[ax][1] = l.y, n.lo[ax][2] = l.z, n.lo[ax][3] = l.w;
-        n.hi[ax][0] = h.x, n.hi[ax][1] = h.y, n.hi[ax][2] = h.z, n.hi[ax][3] = h.w;
-    }
-    n.ref[0] = (int32_t)rt_asuint(q[6].x), n.ref[1] = (int32_t)rt_asuint(q[6].y);
-    n.ref[2] = (int32_t)rt_asuint(q[6].z), n.ref[3] = (int32_t)rt_asuint(q[6].w);
-    n.cnt[0] = (int32_t)rt_asuint(q[7].x), n.cnt[1] = (int32_t)rt_asuint(q[7].y);
-    n.cnt[2] = (int32_t)rt_asuint(q[7].z), n.cnt[3] = (int32_t)rt_asuint(q[7].w);
-    return n;
+    return bvh4_unpack(q);
 }
 
 // The four child boxes of a node: entry distance and "passes within [0, tmax]".
@@ -135,6 +138,15 @@ RT_HD void sort4(float* k, int* v)
 
 // Relative width of the window past t* in which other hits are collected.
 #define RT_T2_WINDOW 1.0e-3f
+
+// Search-BVH walk: 1 = one item (node or leaf) per trip (fast_closest_u /
+// fast_any_u), 0 = one node per trip with its leaf children inline.
+#ifndef RT_FAST_WALK_C
+#define RT_FAST_WALK_C 0
+#endif
+#ifndef RT_FAST_WALK_A
+#define RT_FAST_WALK_A 1
+#endif
 
 struct FastHit {
     float t, t2;  // closest M-T hit (-1: none), smallest other hit seen (window-bounded)
@@ -265,13 +277,203 @@ RT_HD bool chain_ok(const RtSceneView& S, const RayK& K, int rec, bool need_t2, 
     }
 }
 
+// ---------------------------------------------------------------------------
+// One-item-per-trip walks. Inner nodes and leaves are both stack items; each
+// trip of the loop loads one item with the same load instructions (an inner
+// node's 8 records or a leaf's 3 * count triangle records, from either array)
+// and then runs the box tests or the triangle tests on it. A wave whose lanes
+// mix nodes and leaves pays one memory round trip per trip instead of one per
+// leaf child of the node (fast_closest above tests a node's leaf children in
+// four divergent branches, each with its own round trip).
+// Item encoding: node index i >= 0; leaf ~((first << 2) | (count - 1)) < 0.
+RT_HD int leaf_item(int first, int count) { return ~((first << 2) | (count - 1)); }
+
+struct ItemRecs {
+    float4_ q[12];
+};
+RT_HD void load_item(const RtSceneView& S, int item, ItemRecs& R)
+{
+    const bool leaf = item < 0;
+    const int v = ~item;
+    const float4_* p = leaf ? S.bvh_tri4 + 3 * (v >> 2) : (const float4_*)(S.bvh4 + item);
+    const int nrec = leaf ? 3 * ((v & 3) + 1) : 8;
+#pragma unroll
+    for (int j = 0; j < 12; j++)
+        if (j < nrec) R.q[j] = p[j];
+}
+RT_HD Bvh4R node_of(const ItemRecs& R)
+{
+    return bvh4_unpack(R.q);
+}
+
+// fast_closest, one item per trip (same result: the set of hits in the final
+// window does not depend on the visiting order).
+template <class STK>
+RT_HD void fast_closest_u(const RtSceneView& S, V3 o, V3 d, STK& stk, FastHit& h, Stats* st)
+{
+    h.t = __builtin_inff();
+    h.t2 = __builtin_inff();
+    h.k = -1;
+    h.tie = false;
+    h.ovf = false;
+    if (st) st->c[RT_STAT_RAYS]++;
+    if (rt_isnan(d.x) || rt_isnan(d.y) || rt_isnan(d.z) || rt_isnan(o.x) || rt_isnan(o.y) || rt_isnan(o.z)) {
+        h.t = -1.0f;
+        return;
+    }
+    const RayB rb = rayb_setup(o, d);
+    int sp = 0;
+    int cur = 0;
+    for (;;) {
+        ItemRecs R;
+        load_item(S, cur, R);
+        if (cur >= 0) {
+            const Bvh4R n = node_of(R);
+            if (st) st->c[RT_STAT_VOL] += 4;
+            float tn[4];
+            bool hit[4];
+            const float tmax = h.t + h.t * RT_T2_WINDOW;
+            box4(n, rb, tmax, tn, hit);
+            float k[4];
+            int v[4];
+            bool ok[4];
+#pragma unroll
+            for (int c = 0; c < 4; c++) {
+                ok[c] = hit[c] && tn[c] <= tmax;
+                k[c] = ok[c] ? tn[c] : __builtin_inff();
+                v[c] = n.cnt[c] > 0 ? leaf_item(n.ref[c], n.cnt[c]) : n.ref[c];
+            }
+            // sort the valid children by entry distance (invalid keys are +inf)
+            int ix[4] = {0, 1, 2, 3};
+            float kk[4] = {k[0], k[1], k[2], k[3]};
+            sort4(kk, ix);
+            int nv = 0;
+#pragma unroll
+            for (int c = 0; c < 4; c++) nv += ok[c] ? 1 : 0;
+            // far children on the stack (nearest of them on top), nearest next
+            bool over = false;
+#pragma unroll
+            for (int j = 3; j >= 1; j--)
+                if (j < nv) {
+                    if (sp == STK::CAP)
+                        over = true;
+                    else
+                        stk.set(sp++, (uint32_t)v[ix[j]], kk[j]);
+                }
+            if (over) {
+                h.ovf = true;
+                return;
+            }
+            if (nv > 0) {
+                cur = v[ix[0]];
+                continue;
+            }
+        } else {
+            const int cnt = ((~cur) & 3) + 1;
+            if (st) st->c[RT_STAT_TRI] += cnt;
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                if (j >= cnt) break;
+                float t;
+                if (tri_test_v(ld3(R.q[3 * j]), ld3(R.q[3 * j + 1]), ld3(R.q[3 * j + 2]), o, d, t)) {
+                    if (t < h.t) {
+                        h.t2 = h.t;
+                        h.t = t;
+                        h.k = (int)rt_asuint(R.q[3 * j].w);
+                        h.leaf = (int)rt_asuint(R.q[3 * j + 1].w);
+                        h.tie = false;
+                    } else if (t == h.t) {
+                        h.tie = true;
+                        h.t2 = t;
+                    } else if (t < h.t2) {
+                        h.t2 = t;
+                    }
+                }
+            }
+        }
+        // pop, dropping entries the window has closed behind
+        const float tmax = h.t + h.t * RT_T2_WINDOW;
+        cur = 0x7fffffff;
+        while (sp > 0) {
+            --sp;
+            if (stk.key(sp) <= tmax) {
+                cur = (int)stk.rec(sp);
+                break;
+            }
+        }
+        if (cur == 0x7fffffff) break;
+    }
+    if (h.k < 0) h.t = -1.0f;
+}
+
+// fast_query_any, one item per trip.
+template <class STK>
+RT_HD int fast_any_u(const RtSceneView& S, V3 o, V3 d, STK& stk, Stats* st)
+{
+    if (st) st->c[RT_STAT_ANY_RAYS]++;
+    if (rt_isnan(d.x) || rt_isnan(d.y) || rt_isnan(d.z) || rt_isnan(o.x) || rt_isnan(o.y) || rt_isnan(o.z)) return 0;
+    const RayB rb = rayb_setup(o, d);
+    RayK K;
+    bool kset = false;
+    int sp = 0;
+    int cur = 0;
+    for (;;) {
+        ItemRecs R;
+        load_item(S, cur, R);
+        bool have = false;
+        if (cur >= 0) {
+            const Bvh4R n = node_of(R);
+            if (st) st->c[RT_STAT_ANY_VOL] += 4;
+            float tn[4];
+            bool hit[4];
+            box4(n, rb, __builtin_inff(), tn, hit);
+            bool over = false;
+#pragma unroll
+            for (int c = 0; c < 4; c++) {
+                if (!hit[c]) continue;
+                const int it = n.cnt[c] > 0 ? leaf_item(n.ref[c], n.cnt[c]) : n.ref[c];
+                if (!have) {
+                    cur = it;
+                    have = true;
+                } else if (sp == STK::CAP) {
+                    over = true;
+                } else {
+                    stk.set(sp++, (uint32_t)it, 0.0f);
+                }
+            }
+            if (over) return -1;
+        } else {
+            const int cnt = ((~cur) & 3) + 1;
+            if (st) st->c[RT_STAT_ANY_TRI] += cnt;
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                if (j >= cnt) break;
+                float t;
+                if (tri_test_v(ld3(R.q[3 * j]), ld3(R.q[3 * j + 1]), ld3(R.q[3 * j + 2]), o, d, t)) {
+                    if (!kset) {
+                        ray_setup(o, d, K);
+                        kset = true;
+                    }
+                    if (chain_ok(S, K, (int)rt_asuint(R.q[3 * j + 1].w), false, 0.0f, st)) return 1;
+                }
+            }
+        }
+        if (have) continue;
+        if (sp == 0) return 0;
+        cur = (int)stk.rec(--sp);
+    }
+}
+
 // Closest-hit query answered through the BVH and verified against the
 // octree. Returns false when the answer must come from the exact walk.
-template <class STK>
+template <class STK, int WALK = RT_FAST_WALK_C>
 RT_HD bool fast_query_closest(const RtSceneView& S, V3 o, V3 d, STK& stk, float& t_out, int& k_out, Stats* st)
 {
     FastHit h;
-    fast_closest(S, o, d, stk, h, st);
+    if (WALK == 1)
+        fast_closest_u(S, o, d, stk, h, st);
+    else
+        fast_closest(S, o, d, stk, h, st);
     if (h.ovf) return false;
     if (h.k < 0) {  // no M-T hit anywhere: the reference finds none either
         t_out = -1.0f;
@@ -291,9 +493,10 @@ RT_HD bool fast_query_closest(const RtSceneView& S, V3 o, V3 d, STK& stk, float&
 // Occlusion query (exact; needs no fallback): is there an M-T-hit triangle
 // whose octree leaf the reference's walk reaches? 1 / 0; -1 when the
 // bounded stack overflowed (answer unknown).
-template <class STK>
+template <class STK, int WALK = RT_FAST_WALK_A>
 RT_HD int fast_query_any(const RtSceneView& S, V3 o, V3 d, STK& stk, Stats* st)
 {
+    if (WALK == 1) return fast_any_u(S, o, d, stk, st);
     if (st) st->c[RT_STAT_ANY_RAYS]++;
     if (rt_isnan(d.x) || rt_isnan(d.y) || rt_isnan(d.z) || rt_isnan(o.x) || rt_isnan(o.y) || rt_isnan(o.z)) return 0;
     const RayB rb = rayb_setup(o, d);

@@ -1,0 +1,275 @@
+// rt_quad.h — search-BVH queries walked by a quad of lanes (gfx950 only).
+//
+// The one-lane walks of rt_fast.h execute, for every trip of the wave, the
+// box tests of a node and (unrolled) the Moller-Trumbore tests of all of its
+// leaf children: whenever any of the 64 lanes needs a branch the whole wave
+// pays for it, so a node visit costs ~2000 wave instructions (~3-4 us per
+// visit measured on an idle MI355X, tools/chunk_trace.py). A query's latency
+// sets how fast a pixel's 64 x (bounces + 1) dependent steps can go, which
+// bounds the frame when few pixels are left (and at 8 GPUs, always).
+//
+// Here four consecutive lanes (a quad) walk one query together:
+//  * inner node: lane j loads child j (two 16-B loads of its 32-B record,
+//    rt_device.h Bvh4Child) and runs one box test; the quad ranks the hits
+//    by entry distance through DPP quad permutes, the nearest becomes the
+//    next item and the others are pushed (each lane writes its own entry);
+//  * leaf: lane j runs the reference's Moller-Trumbore test on triangle j;
+//    the quad reduces (closest, second, tie) with DPP.
+// Every trip is one memory round trip and ~1/10 of the instructions. The
+// answer is the one rt_fast.h defines (same window, same tie / second-hit
+// bookkeeping, same verification), so the query falls back to the exact
+// octree walk in exactly the same cases.
+//
+// Contract: all four lanes of a quad call these functions together with the
+// same ray, in quad-uniform control flow (DPP reads the other lanes).
+#pragma once
+
+#include "rt_fast.h"
+
+namespace rtk {
+
+#define RT_QX1 0xB1  // quad_perm [1,0,3,2]: lane j ^ 1
+#define RT_QX2 0x4E  // quad_perm [2,3,0,1]: lane j ^ 2
+#define RT_QX3 0x1B  // quad_perm [3,2,1,0]: lane j ^ 3
+
+template <int CTRL>
+__device__ __forceinline__ int qdpp(int v)
+{
+    return __builtin_amdgcn_mov_dpp(v, CTRL, 0xF, 0xF, true);
+}
+template <int CTRL>
+__device__ __forceinline__ float qdppf(float v)
+{
+    return __int_as_float(qdpp<CTRL>(__float_as_int(v)));
+}
+// Is lane sub ^ x below lane sub?
+__device__ __forceinline__ bool s_lower(int sub, int x) { return (sub ^ x) < sub; }
+// OR over the quad (used to broadcast the value of the one lane that holds it, others 0)
+__device__ __forceinline__ int qor(int v)
+{
+    v |= qdpp<RT_QX1>(v);
+    return v | qdpp<RT_QX2>(v);
+}
+__device__ __forceinline__ int qsum(int v)
+{
+    v += qdpp<RT_QX1>(v);
+    return v + qdpp<RT_QX2>(v);
+}
+
+// Per-quad stack in LDS: entry i of quad q at [i * QPB + q].
+template <int N, int QPB>
+struct QuadStack {
+    static constexpr int CAP = N;
+    uint32_t* r;  // base + q
+    float* k;
+    __device__ __forceinline__ uint32_t rec(int i) const { return r[i * QPB]; }
+    __device__ __forceinline__ float key(int i) const { return k[i * QPB]; }
+    __device__ __forceinline__ void set(int i, uint32_t rv, float kv)
+    {
+        r[i * QPB] = rv;
+        k[i * QPB] = kv;
+    }
+};
+
+// Lane `sub`'s child of inner node `node`: box test within [0, tmax].
+struct QChild {
+    int item;  // node index or leaf item (rt_fast.h leaf_item)
+    bool ok;
+    float tn;
+};
+__device__ __forceinline__ QChild quad_child(const RtSceneView& S, int node, int sub, const RayB& rb, float tmax)
+{
+    const float4_* p = (const float4_*)(S.bvh4 + node) + 2 * sub;
+    const float4_ a = p[0], b = p[1];
+    const int ref = (int)rt_asuint(b.z), cnt = (int)rt_asuint(b.w);
+    const float mn[3] = {a.x, a.y, a.z}, mx[3] = {a.w, b.x, b.y};
+    QChild c;
+    c.ok = cnt >= 0 && box_hit(mn, mx, rb, tmax, c.tn) && c.tn <= tmax;
+    c.item = cnt > 0 ? leaf_item(ref, cnt) : ref;
+    return c;
+}
+
+// Lane `sub`'s triangle of a leaf item: Moller-Trumbore (the reference's
+// arithmetic). Returns t (+inf when the lane has no triangle or no hit).
+__device__ __forceinline__ float quad_tri(const RtSceneView& S, int item, int sub, V3 o, V3 d, int& k, int& leaf)
+{
+    const int v = ~item;
+    const int first = v >> 2, cnt = (v & 3) + 1;
+    float tv = __builtin_inff();
+    k = -1;
+    leaf = -1;
+    if (sub < cnt) {
+        const float4_* p = S.bvh_tri4 + 3 * (first + sub);
+        const float4_ a = p[0], e1 = p[1], e2 = p[2];
+        float t;
+        if (tri_test_v(ld3(a), ld3(e1), ld3(e2), o, d, t)) {
+            tv = t;
+            k = (int)rt_asuint(a.w);
+            leaf = (int)rt_asuint(e1.w);
+        }
+    }
+    return tv;
+}
+
+// fast_closest (rt_fast.h) walked by a quad. h is quad-uniform on return.
+template <class QSTK>
+__device__ void quad_closest(const RtSceneView& S, V3 o, V3 d, QSTK& stk, int sub, FastHit& h, Stats* st)
+{
+    h.t = __builtin_inff();
+    h.t2 = __builtin_inff();
+    h.k = -1;
+    h.leaf = -1;
+    h.tie = false;
+    h.ovf = false;
+    if (st && sub == 0) st->c[RT_STAT_RAYS]++;
+    if (rt_isnan(d.x) || rt_isnan(d.y) || rt_isnan(d.z) || rt_isnan(o.x) || rt_isnan(o.y) || rt_isnan(o.z)) {
+        h.t = -1.0f;
+        return;
+    }
+    const RayB rb = rayb_setup(o, d);
+    int sp = 0;
+    int cur = 0;
+    for (;;) {
+        if (cur >= 0) {
+            if (st && sub == 0) st->c[RT_STAT_VOL] += 4;
+            const float tmax = h.t + h.t * RT_T2_WINDOW;
+            const QChild c = quad_child(S, cur, sub, rb, tmax);
+            const float key = c.ok ? c.tn : __builtin_inff();
+            // rank by (key, lane): the nearest hit child has rank 0
+            const float k1 = qdppf<RT_QX1>(key), k2 = qdppf<RT_QX2>(key), k3 = qdppf<RT_QX3>(key);
+            const int s1 = sub ^ 1, s2 = sub ^ 2, s3 = sub ^ 3;
+            const int rank = (k1 < key || (k1 == key && s1 < sub) ? 1 : 0) + (k2 < key || (k2 == key && s2 < sub) ? 1 : 0) +
+                             (k3 < key || (k3 == key && s3 < sub) ? 1 : 0);
+            const int nv = qsum(c.ok ? 1 : 0);
+            if (sp + nv - 1 > QSTK::CAP) {
+                h.ovf = true;
+                return;
+            }
+            // far children on the stack, nearest of them on top (rank 1 at sp + nv - 2)
+            if (c.ok && rank > 0) stk.set(sp + nv - 1 - rank, (uint32_t)c.item, key);
+            if (nv > 0) {
+                sp += nv - 1;
+                cur = qor(c.ok && rank == 0 ? c.item : 0);
+                continue;
+            }
+        } else {
+            if (st && sub == 0) st->c[RT_STAT_TRI] += ((~cur) & 3) + 1;
+            int k, leaf;
+            const float tv = quad_tri(S, cur, sub, o, d, k, leaf);
+            // quad (smallest, second smallest) of the lanes' hit distances
+            float m1 = tv, m2 = __builtin_inff();
+            {
+                const float o1 = qdppf<RT_QX1>(m1), o2 = qdppf<RT_QX1>(m2);
+                const float n1 = __builtin_fminf(m1, o1), n2 = __builtin_fminf(__builtin_fmaxf(m1, o1), __builtin_fminf(m2, o2));
+                m1 = n1, m2 = n2;
+            }
+            {
+                const float o1 = qdppf<RT_QX2>(m1), o2 = qdppf<RT_QX2>(m2);
+                const float n1 = __builtin_fminf(m1, o1), n2 = __builtin_fminf(__builtin_fmaxf(m1, o1), __builtin_fminf(m2, o2));
+                m1 = n1, m2 = n2;
+            }
+            if (m1 < h.t) {
+                // the lowest lane holding m1 (a second one would make m2 == m1: a tie)
+                const bool mine = tv == m1 && !(qdppf<RT_QX1>(tv) == m1 && s_lower(sub, 1)) &&
+                                  !(qdppf<RT_QX2>(tv) == m1 && s_lower(sub, 2)) && !(qdppf<RT_QX3>(tv) == m1 && s_lower(sub, 3));
+                h.t2 = __builtin_fminf(h.t, m2);
+                h.t = m1;
+                h.k = qor(mine ? k : 0);
+                h.leaf = qor(mine ? leaf : 0);
+                h.tie = m2 == m1;
+            } else if (m1 == h.t && m1 < __builtin_inff()) {
+                h.tie = true;
+                h.t2 = m1;
+            } else {
+                h.t2 = __builtin_fminf(h.t2, m1);
+            }
+        }
+        // pop, dropping entries the window has closed behind
+        const float tmax = h.t + h.t * RT_T2_WINDOW;
+        cur = 0x7fffffff;
+        while (sp > 0) {
+            --sp;
+            if (stk.key(sp) <= tmax) {
+                cur = (int)stk.rec(sp);
+                break;
+            }
+        }
+        if (cur == 0x7fffffff) break;
+    }
+    if (h.k < 0) h.t = -1.0f;
+}
+
+// fast_query_closest by a quad: true with (t, k) when answered, false when
+// the exact walk must answer (same cases as the one-lane walk).
+template <class QSTK>
+__device__ bool quad_query_closest(const RtSceneView& S, V3 o, V3 d, QSTK& stk, int sub, float& t_out, int& k_out,
+                                   Stats* st)
+{
+    FastHit h;
+    quad_closest(S, o, d, stk, sub, h, st);
+    if (h.ovf) return false;
+    if (h.k < 0) {
+        t_out = -1.0f;
+        k_out = -1;
+        return true;
+    }
+    if (h.tie) return false;
+    // chain check on lane 0, broadcast
+    int ok = 0;
+    if (sub == 0) {
+        RayK K;
+        ray_setup(o, d, K);
+        const float t2 = __builtin_fminf(h.t2, h.t + h.t * RT_T2_WINDOW);
+        ok = chain_ok(S, K, h.leaf, true, t2, st) ? 1 : 0;
+    }
+    if (!qor(ok)) return false;
+    t_out = h.t;
+    k_out = h.k;
+    return true;
+}
+
+// fast_query_any by a quad: 1 / 0, -1 when the bounded stack overflowed.
+template <class QSTK>
+__device__ int quad_query_any(const RtSceneView& S, V3 o, V3 d, QSTK& stk, int sub, Stats* st)
+{
+    if (st && sub == 0) st->c[RT_STAT_ANY_RAYS]++;
+    if (rt_isnan(d.x) || rt_isnan(d.y) || rt_isnan(d.z) || rt_isnan(o.x) || rt_isnan(o.y) || rt_isnan(o.z)) return 0;
+    const RayB rb = rayb_setup(o, d);
+    int sp = 0;
+    int cur = 0;
+    for (;;) {
+        bool have = false;
+        if (cur >= 0) {
+            if (st && sub == 0) st->c[RT_STAT_ANY_VOL] += 4;
+            const QChild c = quad_child(S, cur, sub, rb, __builtin_inff());
+            const int okb = c.ok ? 1 : 0;
+            // exclusive prefix of the ok lanes: the first one is next, the rest are pushed
+            const int o1 = qdpp<RT_QX1>(okb), o2 = qdpp<RT_QX2>(okb), o3 = qdpp<RT_QX3>(okb);
+            const int pre = (s_lower(sub, 1) ? o1 : 0) + (s_lower(sub, 2) ? o2 : 0) + (s_lower(sub, 3) ? o3 : 0);
+            const int nv = okb + o1 + o2 + o3;
+            if (sp + nv - 1 > QSTK::CAP) return -1;
+            if (c.ok && pre > 0) stk.set(sp + pre - 1, (uint32_t)c.item, 0.0f);
+            if (nv > 0) {
+                sp += nv - 1;
+                cur = qor(c.ok && pre == 0 ? c.item : 0);
+                have = true;
+            }
+        } else {
+            if (st && sub == 0) st->c[RT_STAT_ANY_TRI] += ((~cur) & 3) + 1;
+            int k, leaf;
+            const float tv = quad_tri(S, cur, sub, o, d, k, leaf);
+            int hit = 0;
+            if (tv < __builtin_inff()) {
+                RayK K;
+                ray_setup(o, d, K);
+                hit = chain_ok(S, K, leaf, false, 0.0f, st) ? 1 : 0;
+            }
+            if (qor(hit)) return 1;
+        }
+        if (have) continue;
+        if (sp == 0) return 0;
+        cur = (int)stk.rec(--sp);
+    }
+}
+
+}  // namespace rtk

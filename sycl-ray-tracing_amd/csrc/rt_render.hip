@@ -25,6 +25,7 @@
 
 #include "rt_context.h"
 #include "rt_wave.h"
+#include "rt_quad.h"
 
 #define HIPCHK(ctx, expr)                                                                         \
     do {                                                                                          \
@@ -85,6 +86,7 @@ struct Backend {
     DevBuf nodes, tri4, prim2k, mat_idx, mats, emissive, spheres, env, env_lum, cdf;
     DevBuf bvh4, bvh_tri4, parent, leaf_of, cdf_row, cdf_coarse;
     DevBuf stats;     // RT_STAT_COUNT u64
+    DevBuf iterq;     // stats renders: per-iteration {queries, live slots} (RT_ITER_LOG)
     DevBuf wave;      // path state, pending records, results, queues, lists
     DevBuf counters;  // C_COUNT int32
     DevBuf xy;        // pixel list (rt_render_pixels)
@@ -256,6 +258,8 @@ __global__ __launch_bounds__(256, 3) void k_step(rtk::WaveView W, int par, unsig
     }
     shard_prefix(cnt, RT_QSHARDS, [&](int j) { return ac_at(par, j); }, s_pre);
     const int n = s_pre[RT_QSHARDS];
+    if (STATS && W.iterq && blockIdx.x == 0 && threadIdx.x == 0 && W.iter < RT_MAX_TIMED_ITERS)
+        W.iterq[2 * W.iter + 1] = n;
     rtk::Stats st;
     if (STATS)
         for (int i = 0; i < RT_STAT_COUNT; i++) st.c[i] = 0;
@@ -297,6 +301,7 @@ __global__ __launch_bounds__(256, 3) void k_step(rtk::WaveView W, int par, unsig
 #define RT_LDS_CAP_CLOSEST 16   // exact walks: key + record (windows are powers of two)
 #define RT_LDS_CAP_ANY 32
 #define RT_REFILL 16
+#define RT_QSTACK 32            // quad walks (rt_quad.h): stack entries per quad (item + key, 64 quads per block)
 
 // Search-BVH stack of a fast query: entries [0, N) in LDS (entry i of
 // thread t at [i * 256 + t]: a wave at equal depth touches 64 consecutive
@@ -480,10 +485,9 @@ __global__ __launch_bounds__(256, 4) void k_trace(rtk::WaveView W, int par, unsi
         return;
     }
 
-    // fast roles
-    const size_t gl = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    FastStack<RT_LDS_CAP_FAST, RT_SPILL_FAST> stk{s_lds + threadIdx.x, (float*)s_lds + RT_LDS_CAP_FAST * 256 + threadIdx.x,
-                                                  W.fspill_r + gl * RT_SPILL_FAST, W.fspill_k + gl * RT_SPILL_FAST};
+    // fast roles: a quad of lanes per query (rt_quad.h), 16 queries per wave
+    const int sub = (int)(threadIdx.x & 3);
+    rtk::QuadStack<RT_QSTACK, 64> stk{s_lds + (threadIdx.x >> 2), (float*)s_lds + RT_QSTACK * 64 + (threadIdx.x >> 2)};
     // queue segments (kind-major, then shard): prefix table in LDS
     shard_prefix(cnt, rtk::RK_COUNT * RT_QSHARDS,
                  [&](int j) { return qc_at(par, j / RT_QSHARDS, j % RT_QSHARDS); }, s_pre);
@@ -491,6 +495,8 @@ __global__ __launch_bounds__(256, 4) void k_trace(rtk::WaveView W, int par, unsi
     const int c0 = s_pre[rtk::RK_CONT * RT_QSHARDS], a0 = s_pre[rtk::RK_ESH * RT_QSHARDS];
     const int nc = s_pre[(last_kind + 1) * RT_QSHARDS] - c0;
     const int na = W.any_rays ? s_pre[(rtk::RK_BENV + 1) * RT_QSHARDS] - a0 : 0;
+    if (STATS && W.iterq && b == nbe_c + nbe_a && threadIdx.x == 0 && W.iter < RT_MAX_TIMED_ITERS)
+        W.iterq[2 * W.iter] = nc + na + ec + ea;
     const int fb0 = nbe_c + nbe_a, nbf = (int)gridDim.x - fb0;
     const int nbc = split_blocks(nbf, nc, na);
     const bool closest = b - fb0 < nbc;
@@ -501,8 +507,8 @@ __global__ __launch_bounds__(256, 4) void k_trace(rtk::WaveView W, int par, unsi
     const int total = closest ? nc : na;
     int32_t* fbn = cnt + (closest ? C_FBC0 : C_FBA0) + (par ^ 1);
     rtk::RayRec* fbl = closest ? W.fb_c[par ^ 1] : W.fb_a[par ^ 1];
-    for (int base = wg * 64; base < total; base += wn * 64) {
-        const int idx = base + lane_id();
+    for (int base = wg * 16; base < total; base += wn * 16) {
+        const int idx = base + (lane_id() >> 2);
         bool fail = false;
         rtk::RayRec r;
         uint32_t target = 0;
@@ -523,16 +529,18 @@ __global__ __launch_bounds__(256, 4) void k_trace(rtk::WaveView W, int par, unsi
             if (closest) {
                 float t;
                 int k;
-                if (rtk::fast_query_closest(W.S, rtk::v3of(r.o), rtk::v3of(r.d), stk, t, k, ps))
-                    rtk::finish_closest(W, target, rtk::v3of(r.o), rtk::v3of(r.d), t, k);
-                else
-                    fail = true;
+                if (rtk::quad_query_closest(W.S, rtk::v3of(r.o), rtk::v3of(r.d), stk, sub, t, k, ps)) {
+                    if (sub == 0) rtk::finish_closest(W, target, rtk::v3of(r.o), rtk::v3of(r.d), t, k);
+                } else {
+                    fail = sub == 0;
+                }
             } else {
-                const int a = rtk::fast_query_any(W.S, rtk::v3of(r.o), rtk::v3of(r.d), stk, ps);
-                if (a >= 0)
-                    rtk::finish_any(W, target, a == 1);
-                else
-                    fail = true;
+                const int a = rtk::quad_query_any(W.S, rtk::v3of(r.o), rtk::v3of(r.d), stk, sub, ps);
+                if (a >= 0) {
+                    if (sub == 0) rtk::finish_any(W, target, a == 1);
+                } else {
+                    fail = sub == 0;
+                }
             }
         }
 #ifdef RT_CHUNK_TRACE
@@ -559,7 +567,7 @@ __global__ __launch_bounds__(256, 4) void k_trace(rtk::WaveView W, int par, unsi
                     o[4] = (uint32_t)tsum;
                     o[5] = (uint32_t)(closest ? 1 : 2) | ((xcc & 15u) << 4);
                     o[6] = (uint32_t)(blockIdx.x * 4 + (threadIdx.x >> 6));
-                    o[7] = (uint32_t)min(64, total - base);
+                    o[7] = (uint32_t)min(16, total - base);
                 }
             }
         }
@@ -600,6 +608,64 @@ __global__ __launch_bounds__(256) void k_intersect(RtSceneView S, const float* _
     ot[8] = any ? (int32_t)rt_asuint(h.n.z) : 0;
     ot[9] = (int32_t)rt_asuint(-1.0f);
     ot[10] = (int32_t)rt_asuint(-1.0f);
+}
+
+// Search-BVH query micro-benchmark (tools/query_bench.py): one query per
+// lane, the k_trace stack layout. out_t = t (closest) or 0/1 (any), -2 when
+// the query needs the exact walk.
+template <bool ANY, int WALK>
+__global__ __launch_bounds__(256, 4) void k_query(RtSceneView S, const float4_* __restrict__ rays,
+                                                  float* __restrict__ out_t, int* __restrict__ out_k, int n,
+                                                  uint32_t* spill_r, float* spill_k)
+{
+    __shared__ uint32_t s_lds[RT_LDS_WORDS * 256];
+    const size_t gl = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    FastStack<RT_LDS_CAP_FAST, RT_SPILL_FAST> stk{s_lds + threadIdx.x, (float*)s_lds + RT_LDS_CAP_FAST * 256 + threadIdx.x,
+                                                  spill_r + gl * RT_SPILL_FAST, spill_k + gl * RT_SPILL_FAST};
+    const int stride = (int)(gridDim.x * blockDim.x);
+    for (int i = (int)gl; i < n; i += stride) {
+        const rtk::V3 o = rtk::v3of(rays[2 * i]), d = rtk::v3of(rays[2 * i + 1]);
+        if (ANY) {
+            const int a = rtk::fast_query_any<decltype(stk), WALK>(S, o, d, stk, nullptr);
+            out_t[i] = a < 0 ? -2.0f : (float)a;
+            out_k[i] = 0;
+        } else {
+            float t = 0;
+            int k = 0;
+            const bool ok = rtk::fast_query_closest<decltype(stk), WALK>(S, o, d, stk, t, k, nullptr);
+            out_t[i] = ok ? t : -2.0f;
+            out_k[i] = ok ? k : -2;
+        }
+    }
+}
+
+// The same through the quad walks (rt_quad.h): four lanes per query.
+template <bool ANY>
+__global__ __launch_bounds__(256) void k_query_quad(RtSceneView S, const float4_* __restrict__ rays,
+                                                    float* __restrict__ out_t, int* __restrict__ out_k, int n)
+{
+    __shared__ uint32_t s_lds[2 * RT_QSTACK * 64];
+    const int q = (int)(threadIdx.x >> 2), sub = (int)(threadIdx.x & 3);
+    rtk::QuadStack<RT_QSTACK, 64> stk{s_lds + q, (float*)s_lds + RT_QSTACK * 64 + q};
+    const int stride = (int)(gridDim.x * blockDim.x) >> 2;
+    for (int i = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 2); i < n; i += stride) {
+        const rtk::V3 o = rtk::v3of(rays[2 * i]), d = rtk::v3of(rays[2 * i + 1]);
+        if (ANY) {
+            const int a = rtk::quad_query_any(S, o, d, stk, sub, nullptr);
+            if (sub == 0) {
+                out_t[i] = a < 0 ? -2.0f : (float)a;
+                out_k[i] = 0;
+            }
+        } else {
+            float t = 0;
+            int k = 0;
+            const bool ok = rtk::quad_query_closest(S, o, d, stk, sub, t, k, nullptr);
+            if (sub == 0) {
+                out_t[i] = ok ? t : -2.0f;
+                out_k[i] = ok ? k : -2;
+            }
+        }
+    }
 }
 
 // numerics self-test kernel (tests/test_gpu_parity.py): out[i] = f(in[i])
@@ -752,6 +818,12 @@ static int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounce
     unsigned long long* stats = (unsigned long long*)b->stats.p;
     const bool S = c->stats_enabled;
     if (S) HIPCHK(c, hipMemsetAsync(b->stats.p, 0, b->stats.bytes, s));
+    const char* iter_log = getenv("RT_ITER_LOG");  // per-iteration log: counts (stats renders) / ms (timed renders)
+    if (S && iter_log) {
+        if (int r = ensure(c, b->iterq, RT_MAX_TIMED_ITERS * 8)) return r;
+        HIPCHK(c, hipMemsetAsync(b->iterq.p, 0, RT_MAX_TIMED_ITERS * 8, s));
+        W.iterq = (int32_t*)b->iterq.p;
+    }
     if (getenv("RT_VERBOSE"))
         fprintf(stderr, "[rt] run_wave n=%d cus=%d step_blocks=%d trace_blocks=%d budget=%d wave_bytes=%zu\n", n,
                 dev_cus, step_blocks, trace_blocks, W.budget, need);
@@ -773,6 +845,7 @@ static int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounce
     bool done = false;
     for (; it < max_iters && !done; it++) {
         const int par = it & 1;
+        W.iter = it;
         const bool T = b->timing && it < RT_MAX_TIMED_ITERS;
         if (T)
             for (int k = 0; k < 3; k++)
@@ -843,15 +916,27 @@ static int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounce
         return rt_fail(c, RT_ERR_STATE, "render: wavefront loop did not drain");
     }
     b->last_iters = it;
+    if (S && iter_log) {
+        std::vector<int32_t> h((size_t)2 * RT_MAX_TIMED_ITERS);
+        HIPCHK(c, hipMemcpyAsync(h.data(), b->iterq.p, h.size() * 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(c, hipStreamSynchronize(s));
+        if (FILE* f = fopen((std::string(iter_log) + ".counts").c_str(), "w")) {
+            for (int i = 0; i < it && i < RT_MAX_TIMED_ITERS; i++) fprintf(f, "%d %d %d\n", i, h[2 * i], h[2 * i + 1]);
+            fclose(f);
+        }
+    }
     if (b->timing) {  // per-kernel-class time of this render (HIP events on its stream)
         HIPCHK(c, hipStreamSynchronize(s));
+        FILE* lf = iter_log ? fopen((std::string(iter_log) + ".ms").c_str(), "w") : nullptr;
         for (int i = 0; i < b->last_iters && i < RT_MAX_TIMED_ITERS; i++)
             for (int k = 0; k < 2; k++) {
                 float ms = 0;
                 HIPCHK(c, hipEventElapsedTime(&ms, b->tev[k][i], b->tev[k + 1][i]));
                 b->kms[k] += ms;
                 b->klaunch[k] += 1;
+                if (lf) fprintf(lf, k == 0 ? "%d %.4f" : " %.4f\n", i, ms);
             }
+        if (lf) fclose(lf);
     }
     return RT_OK;
 }
@@ -953,6 +1038,64 @@ extern "C" int rt_device_libm(int device, int fn, const float* in, const float* 
     (void)hipFree(d_in2);
     (void)hipFree(d_out);
     return e == hipSuccess ? RT_OK : RT_ERR_HIP;
+}
+
+// Search-BVH query micro-benchmark: rays[n][8] (origin xyz _, direction xyz _),
+// mode bit 0 = any (else closest), bits 1.. = walk variant; reps timed
+// launches (HIP events), mean ms per launch into *ms.
+extern "C" int rt_device_queries(rt_context* c, int mode, const float* rays, int n, int reps, float* out_t,
+                                 int* out_k, double* ms)
+{
+    if (!c || !c->backend || n <= 0 || reps < 1) return RT_ERR_ARG;
+    Backend* b = be(c);
+    HIPCHK(c, hipSetDevice(c->device));
+    if (c->dirty) {
+        if (int r = rt_backend_upload(c)) return r;
+        c->dirty = false;
+    }
+    int cus = 256;
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device);
+    const int threads = 256, blocks = std::min((n + threads - 1) / threads, cus * 8);
+    const int qblocks = std::min((4 * n + threads - 1) / threads, cus * 16);
+    float4_* d_rays = nullptr;
+    float* d_t = nullptr;
+    int* d_k = nullptr;
+    uint32_t* sr = nullptr;
+    float* sk = nullptr;
+    const size_t lanes = (size_t)blocks * threads;
+    HIPCHK(c, hipMalloc(&d_rays, (size_t)n * 32));
+    HIPCHK(c, hipMalloc(&d_t, (size_t)n * 4));
+    HIPCHK(c, hipMalloc(&d_k, (size_t)n * 4));
+    HIPCHK(c, hipMalloc(&sr, lanes * RT_SPILL_FAST * 4));
+    HIPCHK(c, hipMalloc(&sk, lanes * RT_SPILL_FAST * 4));
+    HIPCHK(c, hipMemcpy(d_rays, rays, (size_t)n * 32, hipMemcpyHostToDevice));
+    auto launch = [&]() {
+        switch (mode) {
+            case 0: hipLaunchKernelGGL((k_query<false, 0>), dim3(blocks), dim3(threads), 0, 0, b->view, d_rays, d_t, d_k, n, sr, sk); break;
+            case 1: hipLaunchKernelGGL((k_query<true, 0>), dim3(blocks), dim3(threads), 0, 0, b->view, d_rays, d_t, d_k, n, sr, sk); break;
+            case 2: hipLaunchKernelGGL((k_query<false, 1>), dim3(blocks), dim3(threads), 0, 0, b->view, d_rays, d_t, d_k, n, sr, sk); break;
+            case 3: hipLaunchKernelGGL((k_query<true, 1>), dim3(blocks), dim3(threads), 0, 0, b->view, d_rays, d_t, d_k, n, sr, sk); break;
+            case 4: hipLaunchKernelGGL((k_query_quad<false>), dim3(qblocks), dim3(threads), 0, 0, b->view, d_rays, d_t, d_k, n); break;
+            default: hipLaunchKernelGGL((k_query_quad<true>), dim3(qblocks), dim3(threads), 0, 0, b->view, d_rays, d_t, d_k, n); break;
+        }
+    };
+    launch();  // warm-up
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipEventRecord(b->ev0, 0));
+    for (int r = 0; r < reps; r++) launch();
+    HIPCHK(c, hipEventRecord(b->ev1, 0));
+    HIPCHK(c, hipEventSynchronize(b->ev1));
+    float t = 0;
+    HIPCHK(c, hipEventElapsedTime(&t, b->ev0, b->ev1));
+    if (ms) *ms = t / reps;
+    HIPCHK(c, hipMemcpy(out_t, d_t, (size_t)n * 4, hipMemcpyDeviceToHost));
+    HIPCHK(c, hipMemcpy(out_k, d_k, (size_t)n * 4, hipMemcpyDeviceToHost));
+    (void)hipFree(d_rays);
+    (void)hipFree(d_t);
+    (void)hipFree(d_k);
+    (void)hipFree(sr);
+    (void)hipFree(sk);
+    return RT_OK;
 }
 
 // Time between the events around the last rt_render_device launch sequence

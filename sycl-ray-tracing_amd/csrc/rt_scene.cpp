@@ -692,24 +692,22 @@ static void collapse_bvh4(const std::vector<BvhNode>& b2, std::vector<Bvh4Node>&
         Bvh4Node nd{};
         for (int i = 0; i < 4; i++) {
             if (i >= m || c[i].cnt < 0) {
-                nd.lox[i] = nd.loy[i] = nd.loz[i] = INFINITY;
-                nd.hix[i] = nd.hiy[i] = nd.hiz[i] = -INFINITY;
-                nd.ref[i] = 0;
-                nd.cnt[i] = -1;
+                for (int a = 0; a < 3; a++) nd.ch[i].lo[a] = INFINITY, nd.ch[i].hi[a] = -INFINITY;
+                nd.ch[i].ref = 0;
+                nd.ch[i].cnt = -1;
                 continue;
             }
-            nd.lox[i] = c[i].mn[0], nd.loy[i] = c[i].mn[1], nd.loz[i] = c[i].mn[2];
-            nd.hix[i] = c[i].mx[0], nd.hiy[i] = c[i].mx[1], nd.hiz[i] = c[i].mx[2];
-            nd.cnt[i] = c[i].cnt;
-            nd.ref[i] = c[i].ref;
+            for (int a = 0; a < 3; a++) nd.ch[i].lo[a] = c[i].mn[a], nd.ch[i].hi[a] = c[i].mx[a];
+            nd.ch[i].cnt = c[i].cnt;
+            nd.ch[i].ref = c[i].ref;
         }
         // inner children get consecutive slots; their subtrees follow depth-first
         Task kids[4];
         int nk = 0;
         for (int i = 0; i < 4; i++)
-            if (nd.cnt[i] == 0) {
-                kids[nk++] = {nd.ref[i], (int)b4.size()};
-                nd.ref[i] = (int)b4.size();
+            if (nd.ch[i].cnt == 0) {
+                kids[nk++] = {nd.ch[i].ref, (int)b4.size()};
+                nd.ch[i].ref = (int)b4.size();
                 b4.emplace_back();
             }
         b4[t.n4] = nd;

@@ -61,6 +61,7 @@ _SIGS = {
     "rt_device_last_kernel_ms": (ctypes.c_double, [P]),
     "rt_device_kernel_timing": (I, [P, I, P, P]),
     "rt_device_last_iterations": (I, [P]),
+    "rt_device_queries": (I, [P, I, P, I, I, P, P, P]),
     # hostsim-only extra
     "rt_hostsim_heap_order": (I, [P, I, P, P]),
 }
