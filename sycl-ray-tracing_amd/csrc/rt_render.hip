@@ -295,13 +295,16 @@ __global__ __launch_bounds__(256, 3) void k_step(rtk::WaveView W, int par, unsig
 //    query whose answer needs the exact walk (or whose stack would overflow)
 //    goes to the fallback list for the next launch, and its slot's r_park
 //    count keeps k_step off the path until the walk has finished.
-#define RT_LDS_WORDS 32         // LDS words per lane of k_trace (32 KB per block of 256)
+#define RT_LDS_WORDS 16         // LDS words per lane of k_trace (16 KB per block of 256)
 #define RT_LDS_CAP_FAST 16      // search-BVH stack: node + key in LDS ...
 #define RT_SPILL_FAST RT_FAST_SPILL  // ... then in the lane's global spill area
-#define RT_LDS_CAP_CLOSEST 16   // exact walks: key + record (windows are powers of two)
-#define RT_LDS_CAP_ANY 32
+#define RT_LDS_CAP_CLOSEST 8    // exact walks: key + record (windows are powers of two)
+#define RT_LDS_CAP_ANY 16
 #define RT_REFILL 16
 #define RT_QSTACK 32            // quad walks (rt_quad.h): stack entries per quad (item + key, 64 quads per block)
+#ifndef RT_TRACE_OCC
+#define RT_TRACE_OCC 6          // k_trace blocks of 256 per CU (VGPR budget 512 / occupancy)
+#endif
 
 // Search-BVH stack of a fast query: entries [0, N) in LDS (entry i of
 // thread t at [i * 256 + t]: a wave at equal depth touches 64 consecutive
@@ -453,7 +456,7 @@ __device__ void exact_any(const rtk::WaveView& W, int par, uint32_t* lds, int la
 }
 
 template <bool STATS>
-__global__ __launch_bounds__(256, 4) void k_trace(rtk::WaveView W, int par, unsigned long long* stats)
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_OCC, 8))) void k_trace(rtk::WaveView W, int par, unsigned long long* stats)
 {
     __shared__ uint32_t s_lds[RT_LDS_WORDS * 256];
     __shared__ int s_pre[rtk::RK_COUNT * RT_QSHARDS + 1];
@@ -618,7 +621,7 @@ __global__ __launch_bounds__(256, 4) void k_query(RtSceneView S, const float4_* 
                                                   float* __restrict__ out_t, int* __restrict__ out_k, int n,
                                                   uint32_t* spill_r, float* spill_k)
 {
-    __shared__ uint32_t s_lds[RT_LDS_WORDS * 256];
+    __shared__ uint32_t s_lds[2 * RT_LDS_CAP_FAST * 256];
     const size_t gl = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     FastStack<RT_LDS_CAP_FAST, RT_SPILL_FAST> stk{s_lds + threadIdx.x, (float*)s_lds + RT_LDS_CAP_FAST * 256 + threadIdx.x,
                                                   spill_r + gl * RT_SPILL_FAST, spill_k + gl * RT_SPILL_FAST};
@@ -788,9 +791,9 @@ static int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounce
     (void)hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, c->device);
     const int threads = 256;
     const int step_blocks = std::min((n + threads - 1) / threads, dev_cus * 8);
-    // k_trace: wave-strided; 4 blocks resident per CU (128 VGPRs: at 5-6 waves/SIMD the
-    // walk spills to scratch or thrashes the vector L1 and runs slower, measured)
-    const int trace_blocks = dev_cus * 8;
+    // k_trace: wave-strided over 2 grid-fills; RT_TRACE_OCC blocks resident per CU (quad
+    // walks: 6 waves/SIMD measured best, 423 vs 374 Msamples/s at 4 and 350 at 8)
+    const int trace_blocks = dev_cus * 2 * RT_TRACE_OCC;
     rtk::WaveView W{};
     W.park_cap = 1 << 16;
     W.shards = RT_QSHARDS;
