@@ -21,7 +21,7 @@ HIPFLAGS := -std=c++17 -O3 -fPIC --offload-arch=$(ARCH) -ffp-contract=off -fno-f
 
 HDRS := $(wildcard $(SRC)/*.h) include/rt_hip.h
 
-all: $(LIB)/librt_hip.so $(LIB)/librt_hostsim.so oracle/liboracle.so build/libm_check
+all: $(LIB)/librt_hip.so $(LIB)/librt_hostsim.so oracle/liboracle.so build/libm_check build/cdf_check
 
 $(OBJ)/%.host.o: $(SRC)/%.cpp $(HDRS)
 	@mkdir -p $(OBJ)
@@ -58,6 +58,10 @@ oracle/liboracle.so: oracle/cpu_oracle.cpp
 build/libm_check: tests/native/libm_check.cpp $(SRC)/rt_libm.h $(SRC)/rt_fp.h
 	@mkdir -p build
 	$(CXX) -std=c++17 -O2 -fopenmp -ffp-contract=off -I$(SRC) $< -o $@ -lm
+
+build/cdf_check: tests/native/cdf_check.cpp $(OBJ)/rt_scene.host.o $(HDRS)
+	@mkdir -p build
+	$(CXX) $(CXXFLAGS) -I$(SRC) $< $(OBJ)/rt_scene.host.o -o $@
 
 # the reference build (container only; needs /root/reference)
 ref:

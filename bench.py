@@ -51,10 +51,10 @@ HBM_PEAK_GBS = 8000.0  # /opt/skills/guides/MI355X_MICROARCH.md (spec)
 # must read. Search-BVH box test 32 B (half of a 64-B node), triangle test
 # 48 B (a, e1, e2 as 3 x 16 B), octree verification slab test 64 B (one
 # record), queue ray 32 B + result 8 B per query; step kernel: material
-# 32 B, env texel 16 B, CDF probe 4 B. (SURVEY.md §8(d)'s model of the
+# 32 B, env texel 16 B, env-CDF fence load 64 B (16 keys; rt_trace.h fence_count). (SURVEY.md §8(d)'s model of the
 # reference's own octree walk — 56 B per child volume, 36 B per triangle —
 # is reported beside it as `ref_model_bytes_per_sample`.)
-BYTES = {"box": 32, "tri": 48, "verify": 64, "ray": 40, "mat": 32, "env": 16, "cdf": 4}
+BYTES = {"box": 32, "tri": 48, "verify": 64, "ray": 40, "mat": 32, "env": 16, "cdf": 64}
 
 
 def algo_bytes(st: dict, kernel: str) -> float:

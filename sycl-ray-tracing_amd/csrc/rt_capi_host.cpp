@@ -38,6 +38,7 @@ RtSceneView rt_host_view(const rt_context* c)
     v.env_lum = c->env_lum.data();
     v.cdf = c->cdf.data();
     v.cdf_row = c->cdf_row.data();
+    v.cdf_fence = c->cdf_fence.empty() ? nullptr : c->cdf_fence.data();
     v.cdf_coarse = c->cdf_coarse.data();
     v.cdf_cw = c->cdf_cw;
     v.n_emissive = (int)c->emissive.size();
@@ -207,8 +208,9 @@ int rt_set_env(rt_context* c, const float* px, int w, int h, int ch, const float
     c->cdf.resize(n);
     rt::env_luminance_cdf(px, w, h, ch, c->env_lum.data(), c->cdf.data());
     if (cdf) c->cdf.assign(cdf, cdf + n);
-    c->cdf_row.resize(h);
+    c->cdf_row.assign((size_t)((h + 15) & ~15), 0.0f);  // (padded: the fence search loads 16 at a time)
     for (int y = 0; y < h; y++) c->cdf_row[y] = c->cdf[(size_t)y * w + w - 1];
+    rt::env_cdf_fences(c->cdf.data(), c->cdf_row.data(), w, h, c->cdf_fence);
     c->cdf_cw = w / 32;
     c->cdf_coarse.resize(std::max<size_t>(1, (size_t)h * c->cdf_cw));
     for (int y = 0; y < h; y++)

@@ -31,6 +31,7 @@ struct rt_context {
     std::vector<float4_> env;     // RGBA, alpha 0
     std::vector<float> env_lum, cdf;
     std::vector<float> cdf_row, cdf_coarse;  // exact copies of CDF entries (rt_trace.h cdf_search)
+    std::vector<float> cdf_fence;            // fence tables of the counting search (empty: not eligible)
     int cdf_cw = 0;
     int ew = 0, eh = 0;
     bool have_env = false;

@@ -78,6 +78,7 @@ struct RtSceneView {
     const float* cdf;
     const float* cdf_row;     // [eh]  cdf of each row's last texel
     const float* cdf_coarse;  // [eh][cdf_cw]  cdf[y*ew + 32j + 31]
+    const float* cdf_fence;   // [1 + eh][272] fence tables (rt_trace.h cdf_search_fence), or null
     int32_t n_emissive, n_spheres, ew, eh;
     int32_t n_tris, chain_monotone, cdf_cw, pad2;  // chain_monotone: see rt_fast.h chain_ok
     // search BVH + octree back-links for the verification walk

@@ -69,6 +69,7 @@ struct QuadStack {
         r[i * QPB] = rv;
         k[i * QPB] = kv;
     }
+    __device__ __forceinline__ void set_rec(int i, uint32_t rv) { r[i * QPB] = rv; }
 };
 
 // Lane `sub`'s child of inner node `node`: box test within [0, tmax].

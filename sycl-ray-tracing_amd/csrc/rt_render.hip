@@ -68,6 +68,7 @@ enum {
     C_PARKA1,
     C_TK_EXACT_C,
     C_TK_EXACT_A,
+    C_TK_TAIL,       // k_tail: next live-list entry to take
     C_SHARDED = 64,  // sharded counters from here (qc_at / ac_at)
 };
 #define RT_QSHARDS 64
@@ -84,7 +85,7 @@ __host__ __device__ __forceinline__ int ac_at(int par, int shard)
 
 struct Backend {
     DevBuf nodes, tri4, prim2k, mat_idx, mats, emissive, spheres, env, env_lum, cdf;
-    DevBuf bvh4, bvh_tri4, parent, leaf_of, cdf_row, cdf_coarse;
+    DevBuf bvh4, bvh_tri4, parent, leaf_of, cdf_row, cdf_coarse, cdf_fence;
     DevBuf stats;     // RT_STAT_COUNT u64
     DevBuf iterq;     // stats renders: per-iteration {queries, live slots} (RT_ITER_LOG)
     DevBuf wave;      // path state, pending records, results, queues, lists
@@ -96,11 +97,12 @@ struct Backend {
     RtSceneView view{};
     int bl_rays = 1, any_rays = 1;
     int last_iters = 0;
+    int tail_iter = -1;     // iteration whose step launch was the tail kernel (-1: none)
     int budget = 1024;  // steps per query per launch before it parks (RT_STEP_BUDGET)
     // optional per-kernel timing: events around each launch of each class
     bool timing = false;
     hipEvent_t tev[3][RT_MAX_TIMED_ITERS] = {};
-    double kms[3] = {0, 0, 0};      // k_trace, k_step, (unused)
+    double kms[3] = {0, 0, 0};      // k_trace, k_step, k_tail
     long klaunch[3] = {0, 0, 0};
 };
 
@@ -585,6 +587,129 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_OC
     flush_stats<STATS>(st, stats);
 }
 
+// ------------------------------------------------------------- tail kernel
+// When few paths are left (the last pixels of a frame are the ones whose
+// samples bounce the most), an iteration costs its slowest query plus its
+// slowest step no matter how few paths it carries, and a pixel's 64 x
+// (bounces + 1) steps are a chain: the frame end is set by that chain. The
+// tail kernel takes the remaining paths in one launch and lets each wave run
+// its own: up to W.tail_paths paths per wave (lanes 0..P-1), step them, trace
+// the rays they emitted from an LDS list with quads, repeat; a wave whose path
+// finishes takes the next one from the live list. No grid-wide step, no
+// launches: each path runs at its own pace.
+// Entry condition (run_wave): no query is parked or waiting for the exact
+// walk, so every path is ready to step; a query the quad walk cannot answer
+// is answered here by the exact walk, inline, by lane 0 of its quad.
+#define RT_TAIL_MAXP 16  // paths per wave at most (5 rays each: 80 per list)
+template <bool STATS>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) void k_tail(rtk::WaveView W, int par, unsigned long long* stats)
+{
+    __shared__ rtk::RayRec s_q[4][2][RT_TAIL_MAXP * rtk::RK_COUNT];  // per wave: closest list, occlusion list
+    __shared__ uint32_t s_stk[2 * RT_QSTACK * 64];
+    __shared__ int s_pre[RT_QSHARDS + 1];
+    int32_t* cnt = W.counters;
+    shard_prefix(cnt, RT_QSHARDS, [&](int j) { return ac_at(par, j); }, s_pre);
+    const int n = s_pre[RT_QSHARDS];
+    rtk::Stats st;
+    if (STATS)
+        for (int i = 0; i < RT_STAT_COUNT; i++) st.c[i] = 0;
+    rtk::Stats* ps = STATS ? &st : nullptr;
+    const int wv = (int)(threadIdx.x >> 6), lane = lane_id(), sub = lane & 3, qd = (int)(threadIdx.x >> 2);
+    rtk::QuadStack<RT_QSTACK, 64> stk{s_stk + qd, (float*)s_stk + RT_QSTACK * 64 + qd};
+    const size_t gl = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    rtk::SpillStack<rtk::QuadStack<RT_QSTACK, 64>> xs{stk, W.spill_r + gl * RT_STACK_CAP, W.spill_k + gl * RT_STACK_CAP};
+    const int P = W.tail_paths;
+    const int last_kind = W.any_rays ? rtk::RK_BL : rtk::RK_BENV;
+    int my = -1;
+    bool drained = false;
+    for (;;) {
+        // refill the wave's pool from the live list
+        const bool need = lane < P && my < 0;
+        const unsigned long long bneed = __ballot(need);
+        if (bneed && !drained) {
+            const int nneed = __popcll(bneed);
+            int base = 0;
+            if (lane == 0) base = atomicAdd(cnt + C_TK_TAIL, nneed);
+            base = __shfl(base, 0);
+            if (base + nneed >= n) drained = true;
+            const int idx = base + __popcll(bneed & ((1ull << lane) - 1ull));
+            if (need && idx < n) {
+                const int sh = shard_find(s_pre, RT_QSHARDS, idx);
+                my = W.act_in[(size_t)sh * W.seg_cap + (idx - s_pre[sh])];
+            }
+        }
+        if (!__any(my >= 0)) break;
+        // step
+        rtk::Emit e;
+        e.mask = 0;
+        e.active = false;
+        if (my >= 0) {
+            rtk::path_step(W, my, e, ps);
+            if (!e.active) my = -1;
+        }
+        // emitted rays -> the wave's LDS lists
+        int nl[2] = {0, 0};
+#pragma unroll
+        for (int k = 0; k < rtk::RK_COUNT; k++) {
+            const bool want = (e.mask >> k) & 1u;
+            const unsigned long long b = __ballot(want);
+            const int l = k <= last_kind ? 0 : 1;
+            if (want) {
+                const int pos = nl[l] + __popcll(b & ((1ull << lane) - 1ull));
+                rtk::RayRec r = e.r[k];
+                r.d.w = rt_asfloat((rt_asuint(r.o.w) << 3) | (uint32_t)k);
+                s_q[wv][l][pos] = r;
+            }
+            nl[l] += __popcll(b);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the lists are read by other lanes
+        __builtin_amdgcn_wave_barrier();
+        // trace: closest list, then occlusion list, 16 queries (quads) per pass
+        for (int l = 0; l < 2; l++) {
+            for (int base = 0; base < nl[l]; base += 16) {
+                const int qi = base + (lane >> 2);
+                if (qi < nl[l]) {
+                    const rtk::RayRec r = s_q[wv][l][qi];
+                    const uint32_t target = rt_asuint(r.d.w);
+                    const rtk::V3 o = rtk::v3of(r.o), d = rtk::v3of(r.d);
+                    bool fail;
+                    if (l == 0) {
+                        float t;
+                        int k;
+                        fail = !rtk::quad_query_closest(W.S, o, d, stk, sub, t, k, ps);
+                        if (!fail && sub == 0) rtk::finish_closest(W, target, o, d, t, k);
+                    } else {
+                        const int a = rtk::quad_query_any(W.S, o, d, stk, sub, ps);
+                        fail = a < 0;
+                        if (!fail && sub == 0) rtk::finish_any(W, target, a == 1);
+                    }
+                    if (fail && sub == 0) {  // the exact octree walk, to completion
+                        if (STATS) st.c[RT_STAT_FALLBACK]++;
+                        xs.f = stk;
+                        if (l == 0) {
+                            rtk::TravC T;
+                            if (rtk::travc_begin(W.S, T, o, d, ps))
+                                while (rtk::travc_step(W.S, T, xs, ps)) {
+                                }
+                            rtk::finish_closest(W, target, T.o, T.d, T.best_t, T.best_k);
+                        } else {
+                            rtk::TravA T;
+                            bool hit = false;
+                            if (rtk::trava_begin(W.S, T, o, d, ps)) {
+                                while (rtk::trava_step(W.S, T, xs, ps)) {
+                                }
+                                hit = T.hit;
+                            }
+                            rtk::finish_any(W, target, hit);
+                        }
+                    }
+                }
+            }
+        }
+    }
+    flush_stats<STATS>(st, stats);
+}
+
 __global__ __launch_bounds__(256) void k_intersect(RtSceneView S, const float* __restrict__ rays, int32_t* __restrict__ out,
                                                    int n)
 {
@@ -722,7 +847,7 @@ void rt_backend_destroy(rt_context* c)
     (void)hipSetDevice(c->device);
     DevBuf* all[] = {&b->nodes, &b->tri4, &b->prim2k, &b->mat_idx, &b->mats, &b->emissive, &b->spheres, &b->env,
                      &b->env_lum, &b->cdf, &b->bvh4, &b->bvh_tri4, &b->parent, &b->leaf_of, &b->cdf_row, &b->cdf_coarse,
-                     &b->stats, &b->wave,
+                     &b->cdf_fence, &b->stats, &b->wave,
                      &b->counters, &b->xy, &b->fb};
     for (DevBuf* d : all)
         if (d->p) (void)hipFree(d->p);
@@ -749,6 +874,7 @@ int rt_backend_upload(rt_context* c)
         (r = upload(c, b->bvh4, c->flat.bvh4)) || (r = upload(c, b->bvh_tri4, c->flat.bvh_tri4)) ||
         (r = upload(c, b->parent, c->flat.parent)) || (r = upload(c, b->leaf_of, c->flat.leaf_of)) ||
         (r = upload(c, b->cdf_row, c->cdf_row)) || (r = upload(c, b->cdf_coarse, c->cdf_coarse)) ||
+        (r = upload(c, b->cdf_fence, c->cdf_fence)) ||
         (r = ensure(c, b->stats, RT_STAT_COUNT * sizeof(unsigned long long))) ||
         (r = ensure(c, b->counters, C_COUNT * sizeof(int32_t))))
         return r;
@@ -765,6 +891,7 @@ int rt_backend_upload(rt_context* c)
     v.cdf = (const float*)b->cdf.p;
     v.cdf_row = (const float*)b->cdf_row.p;
     v.cdf_coarse = (const float*)b->cdf_coarse.p;
+    v.cdf_fence = c->cdf_fence.empty() ? nullptr : (const float*)b->cdf_fence.p;
     v.cdf_cw = c->cdf_cw;
     v.n_emissive = (int)c->emissive.size();
     v.n_spheres = (int)(c->spheres.size() / 2);
@@ -846,6 +973,15 @@ static int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounce
     const long max_iters = 64l * spp * ((long)bounces + 1) + 4096;
     int it = 0;
     bool done = false;
+    // tail kernel (k_tail): RT_TAIL_PATHS paths per wave (0 disables), once at most that many
+    // paths per resident wave are left
+    int tail_p = 4;
+    if (const char* e = getenv("RT_TAIL_PATHS")) tail_p = std::min(RT_TAIL_MAXP, std::max(0, atoi(e)));
+    const int tail_blocks = dev_cus * 3;  // k_tail holds path_step's registers: 3 waves per SIMD
+    W.tail_paths = tail_p;
+    const long tail_max = (long)tail_blocks * 4 * tail_p;
+    bool tail_next = false;
+    b->tail_iter = -1;
     for (; it < max_iters && !done; it++) {
         const int par = it & 1;
         W.iter = it;
@@ -899,19 +1035,40 @@ static int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounce
         }
 #endif
         if (T) HIPCHK(c, hipEventRecord(b->tev[1][it], s));
+        if (tail_next) {
+            // few paths left: if no query waits for the exact walk, the tail
+            // kernel finishes every remaining path in one launch
+            int32_t fbp[8];
+            HIPCHK(c, hipMemcpyAsync(fbp, cnt, sizeof fbp, hipMemcpyDeviceToHost, s));
+            HIPCHK(c, hipStreamSynchronize(s));
+            if (fbp[C_FBC0 + (par ^ 1)] == 0 && fbp[C_FBA0 + (par ^ 1)] == 0 && fbp[C_PARKC0 + (par ^ 1)] == 0 &&
+                fbp[C_PARKA0 + (par ^ 1)] == 0) {
+                HIPCHK(c, hipMemsetAsync(cnt + C_TK_TAIL, 0, 4, s));
+                if (S)
+                    hipLaunchKernelGGL(k_tail<true>, dim3(tail_blocks), dim3(threads), 0, s, W, par, stats);
+                else
+                    hipLaunchKernelGGL(k_tail<false>, dim3(tail_blocks), dim3(threads), 0, s, W, par, stats);
+                if (T) HIPCHK(c, hipEventRecord(b->tev[2][it], s));
+                HIPCHK(c, hipGetLastError());
+                b->tail_iter = it;
+                done = true;
+                continue;
+            }
+        }
         if (S)
             hipLaunchKernelGGL(k_step<true>, dim3(step_blocks), dim3(threads), 0, s, W, par, stats);
         else
             hipLaunchKernelGGL(k_step<false>, dim3(step_blocks), dim3(threads), 0, s, W, par, stats);
         if (T) HIPCHK(c, hipEventRecord(b->tev[2][it], s));
         HIPCHK(c, hipGetLastError());
-        if ((it & 7) == 7) {
+        if ((it & 7) == 7 || tail_next) {
             HIPCHK(c, hipMemcpyAsync(b->h_act, cnt + ac_at(par ^ 1, 0), RT_QSHARDS * RT_CSTRIDE * 4,
                                      hipMemcpyDeviceToHost, s));
             HIPCHK(c, hipStreamSynchronize(s));
             long live = 0;
             for (int j = 0; j < RT_QSHARDS; j++) live += b->h_act[j * RT_CSTRIDE];
             done = live == 0;
+            tail_next = !done && live <= tail_max;
         }
     }
     if (!done) {
@@ -935,9 +1092,15 @@ static int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounce
             for (int k = 0; k < 2; k++) {
                 float ms = 0;
                 HIPCHK(c, hipEventElapsedTime(&ms, b->tev[k][i], b->tev[k + 1][i]));
-                b->kms[k] += ms;
-                b->klaunch[k] += 1;
-                if (lf) fprintf(lf, k == 0 ? "%d %.4f" : " %.4f\n", i, ms);
+                const int cls = (k == 1 && i == b->tail_iter) ? 2 : k;  // the tail kernel: class "other"
+                b->kms[cls] += ms;
+                b->klaunch[cls] += 1;
+                if (lf) {
+                    if (k == 0)
+                        fprintf(lf, "%d %.4f", i, ms);
+                    else
+                        fprintf(lf, " %.4f\n", ms);
+                }
             }
         if (lf) fclose(lf);
     }

@@ -762,6 +762,24 @@ void build_search_bvh(FlatBvh& out)
 }
 
 // ======================================================================= env
+void env_cdf_fences(const float* cdf, const float* row_ends, int w, int h, std::vector<float>& out)
+{
+    out.clear();
+    const size_t n = (size_t)w * h;
+    if (w % 16 != 0 || w - 1 > 4096 || h - 1 > 4096) return;
+    for (size_t i = 0; i < n; i++)
+        if (std::isnan(cdf[i]) || (i > 0 && !(cdf[i] >= cdf[i - 1]))) return;
+    out.assign((size_t)(1 + h) * 272, INFINITY);
+    auto build = [&](const float* a, int m, float* t) {
+        for (int j = 0; j < 16; j++)
+            if (256 * j + 255 < m) t[j] = a[256 * j + 255];
+        for (int j = 0; j < 256; j++)
+            if (16 * j + 15 < m) t[16 + j] = a[16 * j + 15];
+    };
+    build(row_ends, h - 1, out.data());
+    for (int y = 0; y < h; y++) build(cdf + (size_t)y * w, w - 1, out.data() + (size_t)(1 + y) * 272);
+}
+
 void env_luminance_cdf(const float* pix, int w, int h, int channels, float* lum, float* cdf)
 {
     const size_t n = (size_t)w * h;

@@ -75,6 +75,13 @@ void build_search_bvh(FlatBvh& out);
 // lum[i] = (float)(0.3086*r + 0.6094*g + 0.0820*b) in double (image.h:80-85)
 // cdf[i] = cdf[max(i-1,0)] + lum[i] in float, sequential (utils.cpp:126-142)
 void env_luminance_cdf(const float* pix, int w, int h, int channels, float* lum, float* cdf);
+// Fence tables of the counting CDF search (rt_trace.h cdf_search_fence):
+// [1 + h][272] floats, sequence 0 = the row ends, sequence 1 + y = row y;
+// per sequence a[] of length m: 16 block ends at 256 (a[256 j + 255]) then
+// 256 block ends at 16 (a[16 j + 15]), +inf past m. Left empty when the
+// search would not be exact: a NaN or decreasing CDF entry (the reference's
+// probe order then matters), w % 16 != 0, or w or h above 4097.
+void env_cdf_fences(const float* cdf, const float* row_ends, int w, int h, std::vector<float>& out);
 
 // --------------------------------------------------------------- camera
 // Fills view[16] (row-major) and fov_dist for a Camera preset name:

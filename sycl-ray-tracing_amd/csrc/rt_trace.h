@@ -788,8 +788,43 @@ RT_HD Col env_from_dir(const RtSceneView& S, V3 d, Stats* st)  // :520-530
     return env_texel(S, x, y, st);
 }
 
+// Counting form of the reference's search. Its loop (lower = 0, upper =
+// m; while lower < upper: mid = (lower + upper) / 2; value < a[mid] ? upper
+// = mid : lower = mid + 1) never reads a[m] and, on a sequence where the
+// predicate !(value < a[i]) is a prefix (a non-decreasing sequence without
+// NaN, checked on the host — rt_scene.cpp env_cdf_fences), returns the length
+// of that prefix within [0, m): #{i < m : !(value < a[i])}. A NaN value makes
+// every predicate true and returns m, as the loop does. The count is read
+// off three levels of 16 fences, one 64-B load each: block ends at 256 (t[0..16)),
+// block ends at 16 (t[16..272)), then the 16 entries themselves.
+RT_HD int fence_count(const float* a, const float* t, int m, float value)
+{
+    int c = 0;
+    const float* lv[3] = {t, t + 16, a};
+    const int blk[3] = {256, 16, 1};
+#pragma unroll
+    for (int L = 0; L < 3; L++) {
+        const int b = blk[L];
+        const float4_* p = (const float4_*)(lv[L] + c / b);
+        const float4_ q0 = p[0], q1 = p[1], q2 = p[2], q3 = p[3];
+        const float k[16] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w,
+                             q2.x, q2.y, q2.z, q2.w, q3.x, q3.y, q3.z, q3.w};
+        int n = 0;
+#pragma unroll
+        for (int j = 0; j < 16; j++) n += (c + b * (j + 1) - 1 < m && !(value < k[j])) ? 1 : 0;
+        c += n * b;
+    }
+    return c;
+}
+
 RT_HD void cdf_search(const RtSceneView& S, float value, int& x, int& y, Stats* st)  // :532-567
 {
+    if (S.cdf_fence) {
+        y = fence_count(S.cdf_row, S.cdf_fence, S.eh - 1, value);
+        x = fence_count(S.cdf + (size_t)y * S.ew, S.cdf_fence + (size_t)(1 + y) * 272, S.ew - 1, value);
+        if (st) st->c[RT_STAT_CDF] += 6;  // six 64-B fence loads
+        return;
+    }
     int lower = 0, upper = S.eh - 1;
     const int xi = S.ew - 1;
     int probes = 0;

@@ -116,6 +116,7 @@ struct WaveView {
     uint64_t ctrace_t0;
     int32_t* iterq;         // stats renders: [iteration][2] = {queries, live slots} (else null)
     int iter;               // iteration of this launch
+    int tail_paths;         // k_tail: paths per wave
     int shards, seg_cap;    // queues and live lists: `shards` segments of seg_cap entries (device: rt_render.hip)
     const int32_t* act_in;  // active slots this iteration
     int32_t* act_out;

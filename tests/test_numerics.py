@@ -37,3 +37,34 @@ def test_slab_division_identity_host():
         want = a / d
     same = (got.view(np.uint32) == want.view(np.uint32)) | (np.isnan(got) & np.isnan(want))
     assert same.all(), (a[~same][:4], d[~same][:4], got[~same][:4], want[~same][:4])
+
+
+REPO = __import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.abspath(__file__)))
+
+
+def _native(name):
+    import os
+    p = os.path.join(REPO, "build", name)
+    if not os.path.exists(p):
+        import subprocess
+        subprocess.run(["make", "-C", REPO, f"build/{name}"], check=True, capture_output=True)
+    return p
+
+
+def test_cdf_fence_search_matches_reference_loop():
+    """The counting env-CDF search (rt_trace.h fence_count) returns the
+    reference's binary-search result (render_kernel.cpp:532-567) on flat runs,
+    ties, out-of-range, +-inf and NaN values, and the host refuses fence
+    tables for NaN / decreasing CDFs (tests/native/cdf_check.cpp)."""
+    import subprocess
+    r = subprocess.run([_native("cdf_check")], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert " 0 mismatches" in r.stdout
+
+
+def test_libm_restatement_sampled():
+    """rt_libm.h against this host's glibc 2.35 on every 4099th float input
+    (the exhaustive run is tests/native/libm_check.cpp with stride 1)."""
+    import subprocess
+    r = subprocess.run([_native("libm_check"), "4099"], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout + r.stderr
