@@ -57,16 +57,32 @@ HBM_PEAK_GBS = 8000.0  # /opt/skills/guides/MI355X_MICROARCH.md (spec)
 BYTES = {"box": 32, "tri": 48, "verify": 64, "ray": 40, "mat": 32, "env": 16, "cdf": 64}
 
 
+def _query_bytes(g) -> float:
+    return (BYTES["box"] * (g("vol") + g("any_vol")) + BYTES["tri"] * (g("tri") + g("any_tri")) +
+            BYTES["verify"] * g("verify") + BYTES["ray"] * (g("rays") + g("any_rays")))
+
+
+def _step_bytes(g) -> float:
+    return BYTES["mat"] * g("mat") + BYTES["env"] * g("env") + BYTES["cdf"] * g("cdf")
+
+
 def algo_bytes(st: dict, kernel: str) -> float:
-    # k_trace answers every closest-hit and occlusion query; its exact-walk
-    # role (st["fallback"] queries, ~1e-6 of them) shares the box / triangle
-    # counters, so those bytes are booked here too (an overcount of < 0.1%).
+    """Algorithmic bytes of one kernel class over the counted render. The
+    counters are totals over every kernel, plus the tail kernel's share
+    (tail_*): k_trace = query work minus the tail's, k_step = step work
+    minus the tail's, "other" (k_tail) = its query and step work. k_trace's
+    exact-walk role (st["fallback"] queries, ~1e-6 of them) shares the box /
+    triangle counters, so those bytes are booked to it (< 0.1 %)."""
+    tot = lambda k: st[k]  # noqa: E731
+    tail = lambda k: st.get("tail_" + k, 0)  # noqa: E731
+    rest = lambda k: st[k] - st.get("tail_" + k, 0)  # noqa: E731
     if kernel == "trace":
-        return (BYTES["box"] * (st["vol"] + st["any_vol"]) + BYTES["tri"] * (st["tri"] + st["any_tri"]) +
-                BYTES["verify"] * st["verify"] + BYTES["ray"] * (st["rays"] + st["any_rays"]))
+        return _query_bytes(rest)
+    if kernel == "step":
+        return _step_bytes(rest)
     if kernel == "other":
-        return 0.0
-    return BYTES["mat"] * st["mat"] + BYTES["env"] * st["env"] + BYTES["cdf"] * st["cdf"]
+        return _query_bytes(tail) + _step_bytes(tail)
+    return _query_bytes(tot) + _step_bytes(tot)
 
 
 def log(*a):

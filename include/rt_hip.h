@@ -98,7 +98,9 @@ int rt_render_pixels(rt_context* ctx, int width, int height, int samples, int ma
  * normal[3], u, v} with u = v = -1 (unused downstream). */
 int rt_intersect(rt_context* ctx, const float* rays, int n, void* out);
 
-/* Counters of the last render when enabled (RT_STAT_* order, rt_device.h). */
+/* Counters of the last render when enabled (RT_STAT_* order, rt_device.h);
+ * with n up to 2 * RT_STAT_COUNT the second block is the share of the
+ * gfx950 tail kernel (k_tail) in those totals. */
 int rt_set_stats(rt_context* ctx, int enabled);
 int rt_get_stats(const rt_context* ctx, unsigned long long* out, int n);
 /* Average duration (ms) of the last render kernel measured with HIP events. */

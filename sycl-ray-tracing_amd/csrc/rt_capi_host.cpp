@@ -302,7 +302,7 @@ int rt_set_stats(rt_context* c, int enabled)
 int rt_get_stats(const rt_context* c, unsigned long long* out, int n)
 {
     if (!c || !out) return RT_ERR_ARG;
-    for (int i = 0; i < n && i < RT_STAT_COUNT; i++) out[i] = c->stats[i];
+    for (int i = 0; i < n && i < 2 * RT_STAT_COUNT; i++) out[i] = c->stats[i];
     return RT_OK;
 }
 

@@ -40,7 +40,7 @@ struct rt_context {
     bool have_cam = false;
 
     bool stats_enabled = false;
-    unsigned long long stats[RT_STAT_COUNT] = {};
+    unsigned long long stats[2 * RT_STAT_COUNT] = {};  // all kernels, then the gfx950 tail kernel's share
     double last_kernel_ms = 0.0;
 
     bool dirty = true;            // host state changed since the last upload

@@ -37,6 +37,9 @@
 namespace {
 
 #define RT_MAX_TIMED_ITERS 16384
+#ifndef RT_STEP_OCC
+#define RT_STEP_OCC 3  // k_step waves per SIMD
+#endif
 
 struct DevBuf {
     void* p = nullptr;
@@ -86,7 +89,7 @@ __host__ __device__ __forceinline__ int ac_at(int par, int shard)
 struct Backend {
     DevBuf nodes, tri4, prim2k, mat_idx, mats, emissive, spheres, env, env_lum, cdf;
     DevBuf bvh4, bvh_tri4, parent, leaf_of, cdf_row, cdf_coarse, cdf_fence;
-    DevBuf stats;     // RT_STAT_COUNT u64
+    DevBuf stats;     // 2 x RT_STAT_COUNT u64: all kernels, then the tail kernel's share
     DevBuf iterq;     // stats renders: per-iteration {queries, live slots} (RT_ITER_LOG)
     DevBuf wave;      // path state, pending records, results, queues, lists
     DevBuf counters;  // C_COUNT int32
@@ -250,7 +253,7 @@ __global__ __launch_bounds__(256) void k_init(rtk::WaveView W)
 }
 
 template <bool STATS>
-__global__ __launch_bounds__(256, 3) void k_step(rtk::WaveView W, int par, unsigned long long* stats)
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_STEP_OCC, 8))) void k_step(rtk::WaveView W, int par, unsigned long long* stats)
 {
     __shared__ int s_pre[RT_QSHARDS + 1];
     int32_t* cnt = W.counters;
@@ -708,6 +711,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
         }
     }
     flush_stats<STATS>(st, stats);
+    flush_stats<STATS>(st, stats + RT_STAT_COUNT);  // (the tail kernel's share, for per-kernel byte counts)
 }
 
 __global__ __launch_bounds__(256) void k_intersect(RtSceneView S, const float* __restrict__ rays, int32_t* __restrict__ out,
@@ -875,7 +879,7 @@ int rt_backend_upload(rt_context* c)
         (r = upload(c, b->parent, c->flat.parent)) || (r = upload(c, b->leaf_of, c->flat.leaf_of)) ||
         (r = upload(c, b->cdf_row, c->cdf_row)) || (r = upload(c, b->cdf_coarse, c->cdf_coarse)) ||
         (r = upload(c, b->cdf_fence, c->cdf_fence)) ||
-        (r = ensure(c, b->stats, RT_STAT_COUNT * sizeof(unsigned long long))) ||
+        (r = ensure(c, b->stats, 2 * RT_STAT_COUNT * sizeof(unsigned long long))) ||
         (r = ensure(c, b->counters, C_COUNT * sizeof(int32_t))))
         return r;
     RtSceneView v{};

@@ -232,9 +232,12 @@ class RenderKernel:
     def stats(self) -> dict:
         """Counters of the last render (rt_set_stats(True) first), by name."""
         from ._capi import STAT_NAMES
-        out = np.zeros(len(STAT_NAMES), dtype=np.uint64)
-        self.L.rt_get_stats(self.ctx, ptr(out), len(STAT_NAMES))
-        return {k: int(v) for k, v in zip(STAT_NAMES, out)}
+        n = len(STAT_NAMES)
+        out = np.zeros(2 * n, dtype=np.uint64)
+        self.L.rt_get_stats(self.ctx, ptr(out), 2 * n)
+        d = {k: int(v) for k, v in zip(STAT_NAMES, out[:n])}
+        d.update({"tail_" + k: int(v) for k, v in zip(STAT_NAMES, out[n:])})  # the tail kernel's share
+        return d
 
     def kernel_timing(self, enable: int = -1):
         """Per-kernel-class GPU time (HIP events around every launch) since
