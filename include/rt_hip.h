@@ -113,6 +113,16 @@ int rt_mesh_copy(const rt_mesh* m, float* triangles, int* material_indices, floa
 void rt_mesh_free(rt_mesh* m);
 int rt_camera_preset(const char* name, float view[16], float* fov_dist);
 int rt_env_luminance_cdf(const float* pixels, int width, int height, int channels, float* lum, float* cdf);
+/* Utils::read_image_float (utils.cpp:100-124) on a Radiance .hdr file, decoded
+ * like stb_image 2.28 (stb_image.h:7157-7286) and flipped vertically when
+ * flip_y (the reference's default). Call with pixels_rgba == NULL to get the
+ * size, then with a w*h*4 float buffer: RGBA, alpha 0 (utils.cpp:119). */
+int rt_read_hdr(const char* path, int flip_y, int* width, int* height, float* pixels_rgba);
+/* write_image_png (image_io.cpp:165-182): RGBA f32 -> 8 bit exactly as the
+ * reference converts (x*255, clamp to [0,255], truncate), rows flipped when
+ * flip_y, written as a PNG. rt_image_to_rgba8 is the conversion alone. */
+int rt_write_png(const char* path, const float* rgba, int width, int height, int flip_y);
+int rt_image_to_rgba8(const float* rgba, long n_pixels, unsigned char* out);
 /* Octree of a triangle buffer without a device (parity tests). */
 long rt_octree_dump(const float* triangles, int n_triangles, int max_depth, int leaf_max, void* buf, long capacity);
 

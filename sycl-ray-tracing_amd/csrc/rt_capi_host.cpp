@@ -373,3 +373,41 @@ long rt_octree_dump(const float* tris, int n, int max_depth, int leaf_max, void*
 }
 
 }  // extern "C"
+
+// ------------------------------------------------------------- image I/O
+int rt_read_hdr(const char* path, int flip_y, int* width, int* height, float* pixels_rgba)
+{
+    if (!path || !width || !height) return rt_fail(nullptr, RT_ERR_ARG, "rt_read_hdr: bad arguments");
+    int w = 0, h = 0;
+    std::vector<float> rgb;
+    std::string err;
+    if (rt::read_hdr(path, flip_y != 0, w, h, rgb, err)) return rt_fail(nullptr, RT_ERR_IO, "rt_read_hdr: " + err);
+    if (pixels_rgba) {
+        if (*width != w || *height != h) return rt_fail(nullptr, RT_ERR_ARG, "rt_read_hdr: buffer size does not match the image");
+        for (size_t i = 0; i < (size_t)w * h; i++) {  // Color(r, g, b, 0.0f): utils.cpp:114-120
+            pixels_rgba[4 * i] = rgb[3 * i];
+            pixels_rgba[4 * i + 1] = rgb[3 * i + 1];
+            pixels_rgba[4 * i + 2] = rgb[3 * i + 2];
+            pixels_rgba[4 * i + 3] = 0.0f;
+        }
+    }
+    *width = w;
+    *height = h;
+    return RT_OK;
+}
+
+int rt_image_to_rgba8(const float* rgba, long n_pixels, unsigned char* out)
+{
+    if (n_pixels < 0 || (n_pixels > 0 && (!rgba || !out))) return rt_fail(nullptr, RT_ERR_ARG, "rt_image_to_rgba8: bad arguments");
+    rt::rgba8(rgba, (size_t)n_pixels, out);
+    return RT_OK;
+}
+
+int rt_write_png(const char* path, const float* rgba, int width, int height, int flip_y)
+{
+    if (!path || (width > 0 && height > 0 && !rgba)) return rt_fail(nullptr, RT_ERR_ARG, "rt_write_png: bad arguments");
+    std::string err;
+    if (rt::write_png(path, rgba, width, height, flip_y != 0, err)) return rt_fail(nullptr, RT_ERR_IO, "rt_write_png: " + err);
+    return RT_OK;
+}
+

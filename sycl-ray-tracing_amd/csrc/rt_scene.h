@@ -81,6 +81,12 @@ void env_luminance_cdf(const float* pix, int w, int h, int channels, float* lum,
 // 256 block ends at 16 (a[16 j + 15]), +inf past m. Left empty when the
 // search would not be exact: a NaN or decreasing CDF entry (the reference's
 // probe order then matters), w % 16 != 0, or w or h above 4097.
+// Image input / output stages (rt_imageio.cpp): Utils::read_image_float on a
+// Radiance .hdr (stb_image 2.28 decode, flipY), RGB out; write_image_png's
+// 8-bit conversion and a PNG file (flipY).
+int read_hdr(const char* path, bool flip_y, int& width, int& height, std::vector<float>& rgb, std::string& err);
+void rgba8(const float* rgba, size_t n_px, unsigned char* out);
+int write_png(const char* path, const float* rgba, int w, int h, bool flip_y, std::string& err);
 void env_cdf_fences(const float* cdf, const float* row_ends, int w, int h, std::vector<float>& out);
 
 // --------------------------------------------------------------- camera

@@ -7,6 +7,8 @@ Names, argument meaning and mutation semantics follow the reference
   Image                include/image.h:25-178  (RGBA float32, black = (0,0,0,1))
   parse_obj            source/utils.cpp:16-98  -> ParsedOBJ (include/parsed_obj.h)
   compute_env_map_cdf  source/utils.cpp:126-142
+  read_image_float     source/utils.cpp:100-124  (Radiance .hdr, stb_image 2.28 decode, flipY)
+  write_image_png      source/image_io.cpp:165-182
   BVH                  include/bvh.h:211-280, source/bvh.cpp:19-37
   RenderKernel         include/render_kernel.h:21-96
      render()            mutates the image buffer in place (render_kernel.cpp:189-211)
@@ -25,7 +27,8 @@ import numpy as np
 from ._capi import RtError, check, lib, ptr
 
 __all__ = ["Camera", "Image", "ParsedOBJ", "parse_obj", "compute_env_map_cdf", "luminance_of_pixels", "BVH",
-           "RenderKernel", "RtError", "octree_dump", "make_materials"]
+           "RenderKernel", "RtError", "octree_dump", "make_materials", "read_image_float", "write_image_png",
+           "image_to_rgba8"]
 
 
 # ------------------------------------------------------------------ camera
@@ -89,6 +92,35 @@ def compute_env_map_cdf(img: Image) -> np.ndarray:
     cdf = np.empty_like(lum)
     check(lib(), lib().rt_env_luminance_cdf(ptr(img.pixels), img.width, img.height, 4, ptr(lum), ptr(cdf)))
     return cdf
+
+
+def read_image_float(filepath: str, flipY: bool = True) -> Image:
+    """Utils::read_image_float (utils.cpp:100-124) for Radiance .hdr files:
+    RGB decoded like stb_image 2.28, alpha 0, rows flipped when flipY."""
+    L_ = lib()
+    w, h = ctypes.c_int(), ctypes.c_int()
+    check(L_, L_.rt_read_hdr(filepath.encode(), int(flipY), ctypes.byref(w), ctypes.byref(h), None), None,
+          f"read_image_float({filepath})")
+    img = Image(w.value, h.value)
+    check(L_, L_.rt_read_hdr(filepath.encode(), int(flipY), ctypes.byref(w), ctypes.byref(h), ptr(img.pixels)), None,
+          f"read_image_float({filepath})")
+    return img
+
+
+def image_to_rgba8(img: Image) -> np.ndarray:
+    """write_image_png's 8-bit conversion (image_io.cpp:170-177), no flip: [h, w, 4] uint8."""
+    out = np.empty((img.height, img.width, 4), dtype=np.uint8)
+    check(lib(), lib().rt_image_to_rgba8(ptr(img.pixels), img.width * img.height, ptr(out)), None, "image_to_rgba8")
+    return out
+
+
+def write_image_png(image: Image, filename: str, flipY: bool = True) -> bool:
+    """write_image_png (image_io.cpp:165-182): False for an empty image."""
+    if image.width * image.height == 0:
+        return False
+    check(lib(), lib().rt_write_png(filename.encode(), ptr(image.pixels), image.width, image.height, int(flipY)), None,
+          f"write_image_png({filename})")
+    return True
 
 
 # --------------------------------------------------------------------- OBJ

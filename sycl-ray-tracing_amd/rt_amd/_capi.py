@@ -22,7 +22,7 @@ EXPORTS = [
     "rt_set_bvh_preorder", "rt_bvh_dump", "rt_bvh_info", "rt_set_env", "rt_set_camera", "rt_render",
     "rt_render_device", "rt_render_pixels", "rt_intersect", "rt_set_stats", "rt_get_stats", "rt_last_kernel_ms",
     "rt_mesh_load", "rt_mesh_counts", "rt_mesh_copy", "rt_mesh_free", "rt_camera_preset", "rt_env_luminance_cdf",
-    "rt_octree_dump",
+    "rt_octree_dump", "rt_read_hdr", "rt_write_png", "rt_image_to_rgba8",
 ]
 
 P = ctypes.c_void_p
@@ -56,6 +56,9 @@ _SIGS = {
     "rt_camera_preset": (I, [ctypes.c_char_p, P, P]),
     "rt_env_luminance_cdf": (I, [P, I, I, I, P, P]),
     "rt_octree_dump": (L, [P, I, I, I, P, L]),
+    "rt_read_hdr": (I, [ctypes.c_char_p, I, P, P, P]),
+    "rt_write_png": (I, [ctypes.c_char_p, P, I, I, I]),
+    "rt_image_to_rgba8": (I, [P, L, P]),
     # product-only extras
     "rt_device_libm": (I, [I, I, P, P, P, I]),
     "rt_device_last_kernel_ms": (ctypes.c_double, [P]),
