@@ -37,6 +37,7 @@
 namespace {
 
 #define RT_MAX_TIMED_ITERS 16384
+#define RT_MAX_LANES 4  // wavefront lanes (streams) per render (run_wave)
 #ifndef RT_STEP_OCC
 #define RT_STEP_OCC 3  // k_step waves per SIMD
 #endif
@@ -91,12 +92,15 @@ struct Backend {
     DevBuf bvh4, bvh_tri4, parent, leaf_of, cdf_row, cdf_coarse, cdf_fence;
     DevBuf stats;     // 2 x RT_STAT_COUNT u64: all kernels, then the tail kernel's share
     DevBuf iterq;     // stats renders: per-iteration {queries, live slots} (RT_ITER_LOG)
-    DevBuf wave;      // path state, pending records, results, queues, lists
-    DevBuf counters;  // C_COUNT int32
+    DevBuf wave[RT_MAX_LANES];      // per lane: path state, pending records, results, queues, lists
+    DevBuf counters[RT_MAX_LANES];  // per lane: C_COUNT int32
     DevBuf xy;        // pixel list (rt_render_pixels)
     DevBuf fb;        // host-fb staging
-    int32_t* h_act = nullptr;  // pinned host copy of the live-slot counters (sharded)
+    int32_t* h_act[RT_MAX_LANES] = {};     // per lane, pinned: live-slot counters (sharded) + 8 fallback counters
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    hipStream_t ls[RT_MAX_LANES] = {};      // lanes 1.. streams (lane 0 runs on the caller's)
+    hipEvent_t ev_fork = nullptr, ev_join[RT_MAX_LANES] = {}, ev_lane[RT_MAX_LANES] = {};
+    int lanes = 3;                          // RT_LANES (sweep on cfg2: 452 / 499 / 519 / 509 Msamples/s for 1-4)
     RtSceneView view{};
     int bl_rays = 1, any_rays = 1;
     int last_iters = 0;
@@ -104,7 +108,7 @@ struct Backend {
     int budget = 1024;  // steps per query per launch before it parks (RT_STEP_BUDGET)
     // optional per-kernel timing: events around each launch of each class
     bool timing = false;
-    hipEvent_t tev[3][RT_MAX_TIMED_ITERS] = {};
+    hipEvent_t tev[RT_MAX_LANES][3][RT_MAX_TIMED_ITERS] = {};
     double kms[3] = {0, 0, 0};      // k_trace, k_step, k_tail
     long klaunch[3] = {0, 0, 0};
 };
@@ -839,7 +843,14 @@ int rt_backend_create(rt_context* c)
     c->backend = b;
     HIPCHK(c, hipEventCreate(&b->ev0));
     HIPCHK(c, hipEventCreate(&b->ev1));
-    HIPCHK(c, hipHostMalloc((void**)&b->h_act, RT_QSHARDS * RT_CSTRIDE * 4, hipHostMallocDefault));
+    for (int l = 0; l < RT_MAX_LANES; l++) {
+        HIPCHK(c, hipHostMalloc((void**)&b->h_act[l], RT_QSHARDS * RT_CSTRIDE * 4 + 64, hipHostMallocDefault));
+        HIPCHK(c, hipEventCreateWithFlags(&b->ev_lane[l], hipEventDisableTiming));
+        HIPCHK(c, hipEventCreateWithFlags(&b->ev_join[l], hipEventDisableTiming));
+        if (l > 0) HIPCHK(c, hipStreamCreateWithFlags(&b->ls[l], hipStreamNonBlocking));
+    }
+    HIPCHK(c, hipEventCreateWithFlags(&b->ev_fork, hipEventDisableTiming));
+    if (const char* e = getenv("RT_LANES")) b->lanes = std::min(RT_MAX_LANES, std::max(1, atoi(e)));
     if (const char* e = getenv("RT_STEP_BUDGET")) b->budget = std::max(1, atoi(e));
     return RT_OK;
 }
@@ -851,12 +862,21 @@ void rt_backend_destroy(rt_context* c)
     (void)hipSetDevice(c->device);
     DevBuf* all[] = {&b->nodes, &b->tri4, &b->prim2k, &b->mat_idx, &b->mats, &b->emissive, &b->spheres, &b->env,
                      &b->env_lum, &b->cdf, &b->bvh4, &b->bvh_tri4, &b->parent, &b->leaf_of, &b->cdf_row, &b->cdf_coarse,
-                     &b->cdf_fence, &b->stats, &b->wave,
-                     &b->counters, &b->xy, &b->fb};
+                     &b->cdf_fence, &b->stats, &b->xy, &b->fb};
     for (DevBuf* d : all)
         if (d->p) (void)hipFree(d->p);
-    if (b->h_act) (void)hipHostFree(b->h_act);
-    for (auto& row : b->tev)
+    for (int l = 0; l < RT_MAX_LANES; l++)
+        for (DevBuf* d : {&b->wave[l], &b->counters[l]})
+            if (d->p) (void)hipFree(d->p);
+    for (int l = 0; l < RT_MAX_LANES; l++) {
+        if (b->h_act[l]) (void)hipHostFree(b->h_act[l]);
+        if (b->ev_lane[l]) (void)hipEventDestroy(b->ev_lane[l]);
+        if (b->ev_join[l]) (void)hipEventDestroy(b->ev_join[l]);
+        if (b->ls[l]) (void)hipStreamDestroy(b->ls[l]);
+    }
+    if (b->ev_fork) (void)hipEventDestroy(b->ev_fork);
+    for (auto& lane : b->tev)
+        for (auto& row : lane)
         for (hipEvent_t ev : row)
             if (ev) (void)hipEventDestroy(ev);
     if (b->ev0) (void)hipEventDestroy(b->ev0);
@@ -879,9 +899,10 @@ int rt_backend_upload(rt_context* c)
         (r = upload(c, b->parent, c->flat.parent)) || (r = upload(c, b->leaf_of, c->flat.leaf_of)) ||
         (r = upload(c, b->cdf_row, c->cdf_row)) || (r = upload(c, b->cdf_coarse, c->cdf_coarse)) ||
         (r = upload(c, b->cdf_fence, c->cdf_fence)) ||
-        (r = ensure(c, b->stats, 2 * RT_STAT_COUNT * sizeof(unsigned long long))) ||
-        (r = ensure(c, b->counters, C_COUNT * sizeof(int32_t))))
+        (r = ensure(c, b->stats, 2 * RT_STAT_COUNT * sizeof(unsigned long long))))
         return r;
+    for (int l = 0; l < RT_MAX_LANES; l++)
+        if ((r = ensure(c, b->counters[l], C_COUNT * sizeof(int32_t)))) return r;
     RtSceneView v{};
     v.nodes = (const RtNode*)b->nodes.p;
     v.tri4 = (const float4_*)b->tri4.p;
@@ -913,6 +934,23 @@ int rt_backend_upload(rt_context* c)
     return RT_OK;
 }
 
+// One wavefront run over a subset of the launch's pixels (a "lane"): its own
+// path slots, queues, counters and stream. run_wave drives RT_LANES lanes on
+// as many streams (row j of the launch -> lane j % lanes) so that one lane's
+// k_step and the tails of its launches overlap another lane's k_trace.
+struct WaveLane {
+    rtk::WaveView W{};
+    int32_t* lists[2] = {nullptr, nullptr};
+    int32_t* cnt = nullptr;
+    int32_t* h = nullptr;  // pinned readback: ACT shard counts, then 8 FB / PARK counters
+    hipStream_t s = nullptr;
+    hipEvent_t ev = nullptr;
+    int n = 0, it = 0, tail_iter = -1;
+    bool done = false, tail_next = false;
+    int await = 0;  // 0 none, 1 live count, 2 fallback counts (tail entry check)
+    hipEvent_t (*tev)[RT_MAX_TIMED_ITERS] = nullptr;  // [3][RT_MAX_TIMED_ITERS]
+};
+
 // Runs the wavefront loop for n slots of `src` into fb (device, n float4).
 static int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounces, const rtk::PixSrc& src, int n,
                     float4_* fb, hipStream_t s)
@@ -921,191 +959,235 @@ static int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounce
     int dev_cus = 256;
     (void)hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, c->device);
     const int threads = 256;
-    const int step_blocks = std::min((n + threads - 1) / threads, dev_cus * 8);
     // k_trace: wave-strided over 2 grid-fills; RT_TRACE_OCC blocks resident per CU (quad
     // walks: 6 waves/SIMD measured best, 423 vs 374 Msamples/s at 4 and 350 at 8)
     const int trace_blocks = dev_cus * 2 * RT_TRACE_OCC;
-    rtk::WaveView W{};
-    W.park_cap = 1 << 16;
-    W.shards = RT_QSHARDS;
-    W.seg_cap = 64 * (((n + 63) / 64 + RT_QSHARDS - 1) / RT_QSHARDS);  // (append_emit: chunks per shard)
-    W.spill_lanes = dev_cus * 4 * threads;  // exact walks: up to dev_cus * 2 blocks per role
-    W.fspill_lanes = trace_blocks * threads;
-    const size_t need = rtk::wave_carve(nullptr, (size_t)n, W);
-    if (int r = ensure(c, b->wave, need)) return r;
-    rtk::wave_carve((char*)b->wave.p, (size_t)n, W);
-    W.S = b->view;
-    W.cam = c->cam;
-    W.src = src;
-    W.W = w;
-    W.H = h;
-    W.spp = spp;
-    W.bounces = bounces;
-    W.n_slots = n;
-    W.bl_rays = b->bl_rays;
-    W.any_rays = b->any_rays;
-    W.fb = fb;
-    W.budget = b->budget;
-    W.counters = (int32_t*)b->counters.p;
-    int32_t* lists[2] = {(int32_t*)W.act_in, W.act_out};
-    int32_t* cnt = (int32_t*)b->counters.p;
-    unsigned long long* stats = (unsigned long long*)b->stats.p;
     const bool S = c->stats_enabled;
+    unsigned long long* stats = (unsigned long long*)b->stats.p;
     if (S) HIPCHK(c, hipMemsetAsync(b->stats.p, 0, b->stats.bytes, s));
-    const char* iter_log = getenv("RT_ITER_LOG");  // per-iteration log: counts (stats renders) / ms (timed renders)
+    const char* iter_log = getenv("RT_ITER_LOG");  // per-iteration log of lane 0: counts (stats renders) / ms (timed)
     if (S && iter_log) {
         if (int r = ensure(c, b->iterq, RT_MAX_TIMED_ITERS * 8)) return r;
         HIPCHK(c, hipMemsetAsync(b->iterq.p, 0, RT_MAX_TIMED_ITERS * 8, s));
-        W.iterq = (int32_t*)b->iterq.p;
+    }
+    // lanes: rows interleave (row j of the launch -> lane j % lanes); pixel lists split in runs
+    int nl = b->lanes;
+    const int rows = src.xy ? 0 : n / src.W;
+    while (nl > 1 && (n < nl * 65536 || (!src.xy && rows < nl))) nl--;
+    WaveLane L[RT_MAX_LANES];
+    int tail_p = 4;
+    if (const char* e = getenv("RT_TAIL_PATHS")) tail_p = std::min(RT_TAIL_MAXP, std::max(0, atoi(e)));
+    const int tail_blocks = dev_cus * 3;  // k_tail holds path_step's registers: 3 waves per SIMD
+    const long tail_max = (long)tail_blocks * 4 * tail_p / nl;
+    if (nl > 1) {
+        HIPCHK(c, hipEventRecord(b->ev_fork, s));
+        for (int l = 1; l < nl; l++) HIPCHK(c, hipStreamWaitEvent(b->ls[l], b->ev_fork, 0));
+    }
+    for (int l = 0; l < nl; l++) {
+        WaveLane& La = L[l];
+        rtk::PixSrc ls = src;
+        float4_* lfb = fb;
+        int fb_rs = 1;
+        if (nl == 1) {
+            La.n = n;
+        } else if (src.xy) {
+            const int b0 = (int)((long)n * l / nl), b1 = (int)((long)n * (l + 1) / nl);
+            La.n = b1 - b0;
+            ls.xy = src.xy + 2 * (size_t)b0;
+            lfb = fb + b0;
+        } else {
+            La.n = ((rows - l + nl - 1) / nl) * src.W;
+            ls.off = src.off + l * src.stride;
+            ls.stride = nl * src.stride;
+            lfb = fb + (size_t)l * src.W;
+            fb_rs = nl;
+        }
+        La.s = l == 0 ? s : b->ls[l];
+        La.cnt = (int32_t*)b->counters[l].p;
+        La.h = b->h_act[l];
+        La.ev = b->ev_lane[l];
+        La.tev = b->tev[l];
+        rtk::WaveView& W = La.W;
+        W.park_cap = 1 << 16;
+        W.shards = RT_QSHARDS;
+        W.seg_cap = 64 * (((La.n + 63) / 64 + RT_QSHARDS - 1) / RT_QSHARDS);  // (append_emit: chunks per shard)
+        W.spill_lanes = dev_cus * 4 * threads;  // exact walks: up to dev_cus * 2 blocks per role
+        W.fspill_lanes = 0;
+        const size_t need = rtk::wave_carve(nullptr, (size_t)La.n, W);
+        if (int r = ensure(c, b->wave[l], need)) return r;
+        rtk::wave_carve((char*)b->wave[l].p, (size_t)La.n, W);
+        W.S = b->view;
+        W.cam = c->cam;
+        W.src = ls;
+        W.W = w;
+        W.H = h;
+        W.spp = spp;
+        W.bounces = bounces;
+        W.n_slots = La.n;
+        W.bl_rays = b->bl_rays;
+        W.any_rays = b->any_rays;
+        W.fb = lfb;
+        W.fb_rs = fb_rs;
+        W.budget = b->budget;
+        W.counters = La.cnt;
+        W.tail_paths = tail_p;
+        W.iterq = (S && iter_log && l == 0) ? (int32_t*)b->iterq.p : nullptr;
+        La.lists[0] = (int32_t*)W.act_in;
+        La.lists[1] = W.act_out;
+        HIPCHK(c, hipMemsetAsync(La.cnt, 0, C_COUNT * sizeof(int32_t), La.s));
+        HIPCHK(c, hipMemsetAsync(W.r_park, 0, (size_t)La.n * 4, La.s));
+        W.act_in = La.lists[1];
+        W.act_out = La.lists[0];
+        hipLaunchKernelGGL(k_init, dim3((La.n + threads - 1) / threads), dim3(threads), 0, La.s, W);
+        HIPCHK(c, hipGetLastError());
     }
     if (getenv("RT_VERBOSE"))
-        fprintf(stderr, "[rt] run_wave n=%d cus=%d step_blocks=%d trace_blocks=%d budget=%d wave_bytes=%zu\n", n,
-                dev_cus, step_blocks, trace_blocks, W.budget, need);
+        fprintf(stderr, "[rt] run_wave n=%d lanes=%d cus=%d trace_blocks=%d budget=%d\n", n, nl, dev_cus, trace_blocks,
+                b->budget);
 
-    HIPCHK(c, hipMemsetAsync(cnt, 0, C_COUNT * sizeof(int32_t), s));
-    HIPCHK(c, hipMemsetAsync(W.r_park, 0, (size_t)n * 4, s));
-    W.act_in = lists[1];
-    W.act_out = lists[0];
-    hipLaunchKernelGGL(k_init, dim3((n + threads - 1) / threads), dim3(threads), 0, s, W);
-    HIPCHK(c, hipGetLastError());
-
-    // Two launches per iteration (k_trace, k_step); the counter sets they
-    // fill are double-buffered by iteration parity (see C_FBC0).
     // A sample takes at most bounces + 1 iterations without fallbacks; an
     // exact walk delays its path by at least one iteration. The bound only
     // guards against a runaway loop.
     const long max_iters = 64l * spp * ((long)bounces + 1) + 4096;
-    int it = 0;
-    bool done = false;
-    // tail kernel (k_tail): RT_TAIL_PATHS paths per wave (0 disables), once at most that many
-    // paths per resident wave are left
-    int tail_p = 4;
-    if (const char* e = getenv("RT_TAIL_PATHS")) tail_p = std::min(RT_TAIL_MAXP, std::max(0, atoi(e)));
-    const int tail_blocks = dev_cus * 3;  // k_tail holds path_step's registers: 3 waves per SIMD
-    W.tail_paths = tail_p;
-    const long tail_max = (long)tail_blocks * 4 * tail_p;
-    bool tail_next = false;
-    b->tail_iter = -1;
-    for (; it < max_iters && !done; it++) {
-        const int par = it & 1;
-        W.iter = it;
-        const bool T = b->timing && it < RT_MAX_TIMED_ITERS;
+    const size_t act_bytes = RT_QSHARDS * RT_CSTRIDE * 4;
+    auto step_blocks_of = [&](const WaveLane& La) { return std::min((La.n + threads - 1) / threads, dev_cus * 8); };
+    auto launch_trace = [&](WaveLane& La) -> int {
+        rtk::WaveView& W = La.W;
+        const int par = La.it & 1;
+        W.iter = La.it;
+        W.act_in = La.lists[par];
+        W.act_out = La.lists[par ^ 1];
+        const bool T = b->timing && La.it < RT_MAX_TIMED_ITERS;
         if (T)
             for (int k = 0; k < 3; k++)
-                if (!b->tev[k][it]) HIPCHK(c, hipEventCreate(&b->tev[k][it]));
-        // step: reads the list written last iteration (lists[par]) -> lists[par ^ 1]
-        W.act_in = lists[par];
-        W.act_out = lists[par ^ 1];
-        if (T) HIPCHK(c, hipEventRecord(b->tev[0][it], s));
-#ifdef RT_CHUNK_TRACE
-        // debug build: record every chunk of the k_trace launches of the
-        // iterations listed in RT_CHUNK_TRACE_ITERS into RT_CHUNK_TRACE_OUT.<it>
-        bool ct = false;
-        if (const char* e = getenv("RT_CHUNK_TRACE_ITERS")) {
-            char key[32];
-            snprintf(key, sizeof key, ",%d,", it);
-            ct = strstr((std::string(",") + e + ",").c_str(), key) != nullptr;
-        }
-        static uint32_t* d_ct = nullptr;
-        const int ct_cap = 1 << 18;
-        if (ct) {
-            if (!d_ct) HIPCHK(c, hipMalloc(&d_ct, (size_t)ct_cap * 32 + 256));
-            HIPCHK(c, hipMemsetAsync(d_ct, 0, 256, s));
-            W.ctrace_n = (int32_t*)d_ct;
-            W.ctrace = d_ct + 64;
-            W.ctrace_cap = ct_cap;
-            W.ctrace_t0 = 0;
-        }
-#endif
+                if (!La.tev[k][La.it]) HIPCHK(c, hipEventCreate(&La.tev[k][La.it]));
+        if (T) HIPCHK(c, hipEventRecord(La.tev[0][La.it], La.s));
         if (S)
-            hipLaunchKernelGGL(k_trace<true>, dim3(trace_blocks), dim3(threads), 0, s, W, par, stats);
+            hipLaunchKernelGGL(k_trace<true>, dim3(trace_blocks), dim3(threads), 0, La.s, W, par, stats);
         else
-            hipLaunchKernelGGL(k_trace<false>, dim3(trace_blocks), dim3(threads), 0, s, W, par, stats);
-#ifdef RT_CHUNK_TRACE
-        if (ct) {
-            HIPCHK(c, hipStreamSynchronize(s));
-            int32_t nrec = 0;
-            HIPCHK(c, hipMemcpy(&nrec, d_ct, 4, hipMemcpyDeviceToHost));
-            nrec = std::min(nrec, ct_cap);
-            std::vector<uint32_t> h((size_t)nrec * 8);
-            HIPCHK(c, hipMemcpy(h.data(), d_ct + 64, h.size() * 4, hipMemcpyDeviceToHost));
-            const char* outp = getenv("RT_CHUNK_TRACE_OUT");
-            std::string path = std::string(outp ? outp : "chunk_trace") + "." + std::to_string(it);
-            if (FILE* f = fopen(path.c_str(), "wb")) {
-                fwrite(h.data(), 4, h.size(), f);
-                fclose(f);
-            }
-            W.ctrace = nullptr;
-        }
-#endif
-        if (T) HIPCHK(c, hipEventRecord(b->tev[1][it], s));
-        if (tail_next) {
-            // few paths left: if no query waits for the exact walk, the tail
-            // kernel finishes every remaining path in one launch
-            int32_t fbp[8];
-            HIPCHK(c, hipMemcpyAsync(fbp, cnt, sizeof fbp, hipMemcpyDeviceToHost, s));
-            HIPCHK(c, hipStreamSynchronize(s));
-            if (fbp[C_FBC0 + (par ^ 1)] == 0 && fbp[C_FBA0 + (par ^ 1)] == 0 && fbp[C_PARKC0 + (par ^ 1)] == 0 &&
-                fbp[C_PARKA0 + (par ^ 1)] == 0) {
-                HIPCHK(c, hipMemsetAsync(cnt + C_TK_TAIL, 0, 4, s));
-                if (S)
-                    hipLaunchKernelGGL(k_tail<true>, dim3(tail_blocks), dim3(threads), 0, s, W, par, stats);
-                else
-                    hipLaunchKernelGGL(k_tail<false>, dim3(tail_blocks), dim3(threads), 0, s, W, par, stats);
-                if (T) HIPCHK(c, hipEventRecord(b->tev[2][it], s));
-                HIPCHK(c, hipGetLastError());
-                b->tail_iter = it;
-                done = true;
-                continue;
-            }
-        }
-        if (S)
-            hipLaunchKernelGGL(k_step<true>, dim3(step_blocks), dim3(threads), 0, s, W, par, stats);
-        else
-            hipLaunchKernelGGL(k_step<false>, dim3(step_blocks), dim3(threads), 0, s, W, par, stats);
-        if (T) HIPCHK(c, hipEventRecord(b->tev[2][it], s));
+            hipLaunchKernelGGL(k_trace<false>, dim3(trace_blocks), dim3(threads), 0, La.s, W, par, stats);
+        if (T) HIPCHK(c, hipEventRecord(La.tev[1][La.it], La.s));
         HIPCHK(c, hipGetLastError());
-        if ((it & 7) == 7 || tail_next) {
-            HIPCHK(c, hipMemcpyAsync(b->h_act, cnt + ac_at(par ^ 1, 0), RT_QSHARDS * RT_CSTRIDE * 4,
-                                     hipMemcpyDeviceToHost, s));
-            HIPCHK(c, hipStreamSynchronize(s));
-            long live = 0;
-            for (int j = 0; j < RT_QSHARDS; j++) live += b->h_act[j * RT_CSTRIDE];
-            done = live == 0;
-            tail_next = !done && live <= tail_max;
+        return RT_OK;
+    };
+    auto launch_step = [&](WaveLane& La) -> int {
+        const int par = La.it & 1;
+        if (S)
+            hipLaunchKernelGGL(k_step<true>, dim3(step_blocks_of(La)), dim3(threads), 0, La.s, La.W, par, stats);
+        else
+            hipLaunchKernelGGL(k_step<false>, dim3(step_blocks_of(La)), dim3(threads), 0, La.s, La.W, par, stats);
+        if (b->timing && La.it < RT_MAX_TIMED_ITERS) HIPCHK(c, hipEventRecord(La.tev[2][La.it], La.s));
+        HIPCHK(c, hipGetLastError());
+        La.it++;
+        return RT_OK;
+    };
+    auto read_live = [&](WaveLane& La) -> int {  // ACT counts of the next iteration
+        HIPCHK(c, hipMemcpyAsync(La.h, La.cnt + ac_at(La.it & 1, 0), act_bytes, hipMemcpyDeviceToHost, La.s));
+        HIPCHK(c, hipEventRecord(La.ev, La.s));
+        La.await = 1;
+        return RT_OK;
+    };
+    // enqueue up to 8 iterations, then a readback
+    auto issue = [&](WaveLane& La) -> int {
+        for (int k = 0; k < 8 && La.it < max_iters; k++) {
+            if (int r = launch_trace(La)) return r;
+            if (La.tail_next) {  // does any query wait for the exact walk?
+                HIPCHK(c, hipMemcpyAsync(La.h + act_bytes / 4, La.cnt, 8 * 4, hipMemcpyDeviceToHost, La.s));
+                HIPCHK(c, hipEventRecord(La.ev, La.s));
+                La.await = 2;
+                return RT_OK;
+            }
+            if (int r = launch_step(La)) return r;
+            if ((La.it & 7) == 0) break;
+        }
+        return read_live(La);
+    };
+    auto process = [&](WaveLane& La) -> int {
+        HIPCHK(c, hipEventSynchronize(La.ev));
+        const int kind = La.await;
+        La.await = 0;
+        if (kind == 2) {  // (a fallback pending: step, then the live count, checked again next iteration)
+            const int par = La.it & 1;
+            const int32_t* f = La.h + act_bytes / 4;
+            if (f[C_FBC0 + (par ^ 1)] == 0 && f[C_FBA0 + (par ^ 1)] == 0 && f[C_PARKC0 + (par ^ 1)] == 0 &&
+                f[C_PARKA0 + (par ^ 1)] == 0) {
+                // few paths left and none waits: the tail kernel finishes them all
+                HIPCHK(c, hipMemsetAsync(La.cnt + C_TK_TAIL, 0, 4, La.s));
+                if (S)
+                    hipLaunchKernelGGL(k_tail<true>, dim3(tail_blocks), dim3(threads), 0, La.s, La.W, par, stats);
+                else
+                    hipLaunchKernelGGL(k_tail<false>, dim3(tail_blocks), dim3(threads), 0, La.s, La.W, par, stats);
+                if (b->timing && La.it < RT_MAX_TIMED_ITERS) HIPCHK(c, hipEventRecord(La.tev[2][La.it], La.s));
+                HIPCHK(c, hipGetLastError());
+                La.tail_iter = La.it;
+                La.it++;
+                La.done = true;
+                return RT_OK;
+            }
+            if (int r = launch_step(La)) return r;
+            return read_live(La);
+        }
+        long live = 0;
+        for (int j = 0; j < RT_QSHARDS; j++) live += La.h[j * RT_CSTRIDE];
+        La.done = live == 0;
+        La.tail_next = !La.done && live <= tail_max;
+        return RT_OK;
+    };
+    for (int l = 0; l < nl; l++)
+        if (int r = issue(L[l])) return r;
+    for (;;) {
+        bool any = false;
+        for (int l = 0; l < nl; l++) {
+            WaveLane& La = L[l];
+            if (La.await)
+                if (int r = process(La)) return r;
+            if (!La.done) {
+                if (La.it >= max_iters) {
+                    HIPCHK(c, hipStreamSynchronize(La.s));
+                    return rt_fail(c, RT_ERR_STATE, "render: wavefront loop did not drain");
+                }
+                if (int r = issue(La)) return r;
+                any = true;
+            }
+        }
+        if (!any) break;
+    }
+    b->last_iters = 0;
+    for (int l = 0; l < nl; l++) {
+        b->last_iters = std::max(b->last_iters, L[l].it);
+        if (l > 0) {
+            HIPCHK(c, hipEventRecord(b->ev_join[l], b->ls[l]));
+            HIPCHK(c, hipStreamWaitEvent(s, b->ev_join[l], 0));
         }
     }
-    if (!done) {
-        HIPCHK(c, hipStreamSynchronize(s));
-        return rt_fail(c, RT_ERR_STATE, "render: wavefront loop did not drain");
-    }
-    b->last_iters = it;
+    b->tail_iter = L[0].tail_iter;
     if (S && iter_log) {
-        std::vector<int32_t> h((size_t)2 * RT_MAX_TIMED_ITERS);
-        HIPCHK(c, hipMemcpyAsync(h.data(), b->iterq.p, h.size() * 4, hipMemcpyDeviceToHost, s));
+        std::vector<int32_t> hq((size_t)2 * RT_MAX_TIMED_ITERS);
+        HIPCHK(c, hipMemcpyAsync(hq.data(), b->iterq.p, hq.size() * 4, hipMemcpyDeviceToHost, s));
         HIPCHK(c, hipStreamSynchronize(s));
         if (FILE* f = fopen((std::string(iter_log) + ".counts").c_str(), "w")) {
-            for (int i = 0; i < it && i < RT_MAX_TIMED_ITERS; i++) fprintf(f, "%d %d %d\n", i, h[2 * i], h[2 * i + 1]);
+            for (int i = 0; i < L[0].it && i < RT_MAX_TIMED_ITERS; i++) fprintf(f, "%d %d %d\n", i, hq[2 * i], hq[2 * i + 1]);
             fclose(f);
         }
     }
-    if (b->timing) {  // per-kernel-class time of this render (HIP events on its stream)
+    if (b->timing) {  // per-kernel-class time of this render (HIP events on the launch streams)
         HIPCHK(c, hipStreamSynchronize(s));
         FILE* lf = iter_log ? fopen((std::string(iter_log) + ".ms").c_str(), "w") : nullptr;
-        for (int i = 0; i < b->last_iters && i < RT_MAX_TIMED_ITERS; i++)
-            for (int k = 0; k < 2; k++) {
-                float ms = 0;
-                HIPCHK(c, hipEventElapsedTime(&ms, b->tev[k][i], b->tev[k + 1][i]));
-                const int cls = (k == 1 && i == b->tail_iter) ? 2 : k;  // the tail kernel: class "other"
-                b->kms[cls] += ms;
-                b->klaunch[cls] += 1;
-                if (lf) {
-                    if (k == 0)
-                        fprintf(lf, "%d %.4f", i, ms);
-                    else
-                        fprintf(lf, " %.4f\n", ms);
+        for (int l = 0; l < nl; l++)
+            for (int i = 0; i < L[l].it && i < RT_MAX_TIMED_ITERS; i++)
+                for (int k = 0; k < 2; k++) {
+                    float ms = 0;
+                    HIPCHK(c, hipEventElapsedTime(&ms, L[l].tev[k][i], L[l].tev[k + 1][i]));
+                    const int cls = (k == 1 && i == L[l].tail_iter) ? 2 : k;  // the tail kernel: class "other"
+                    b->kms[cls] += ms;
+                    b->klaunch[cls] += 1;
+                    if (lf && l == 0) {
+                        if (k == 0)
+                            fprintf(lf, "%d %.4f", i, ms);
+                        else
+                            fprintf(lf, " %.4f\n", ms);
+                    }
                 }
-            }
         if (lf) fclose(lf);
     }
     return RT_OK;

@@ -69,7 +69,8 @@ struct WaveView {
     int n_slots;
     int bl_rays;            // 0: no primitive has an emissive material -> BRDF->light rays can't contribute
     int any_rays;           // 1: occlusion queries may use the any-hit walk (no analytic spheres)
-    float4_* fb;            // [n_slots] framebuffer values (read-modify-write at pixel end)
+    float4_* fb;            // framebuffer values (read-modify-write at pixel end), see fb_at
+    int fb_rs;              // row sources: framebuffer rows from one slot row to the next (lanes alternate rows)
     // path state
     float4_* p_ro;          // ro.xyz, rng bits
     float4_* p_rd;          // rd.xyz, flags | bounce << 8
@@ -286,6 +287,14 @@ RT_HD bool start_sample(const WaveView& W, int p, PathReg& P, Emit& e)
     }
 }
 
+// Framebuffer entry of slot p: slot rows map to every fb_rs-th framebuffer row.
+RT_HD size_t fb_at(const WaveView& W, int p)
+{
+    if (W.src.xy || W.fb_rs <= 1) return (size_t)p;
+    const int j = p / W.src.W;
+    return (size_t)j * W.fb_rs * W.src.W + (p - j * W.src.W);
+}
+
 RT_HD void finish_pixel(const WaveView& W, int p, PathReg& P)
 {
     const float k = (float)W.spp;
@@ -293,9 +302,10 @@ RT_HD void finish_pixel(const WaveView& W, int p, PathReg& P)
     fin.r /= k;  // Color /= float is a true division (color.h:69-76)
     fin.g /= k;
     fin.b /= k;
-    float4_ px = W.fb[p];
+    float4_& dst = W.fb[fb_at(W, p)];
+    float4_ px = dst;
     tonemap_into(&px.x, fin);
-    W.fb[p] = px;
+    dst = px;
 }
 
 // Path initialisation: seed + 10 warm-up draws (render_kernel.cpp:77-82),
