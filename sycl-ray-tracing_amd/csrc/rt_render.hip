@@ -776,8 +776,8 @@ __global__ __launch_bounds__(256, 4) void k_query(RtSceneView S, const float4_* 
 }
 
 // The same through the quad walks (rt_quad.h): four lanes per query.
-template <bool ANY>
-__global__ __launch_bounds__(256) void k_query_quad(RtSceneView S, const float4_* __restrict__ rays,
+template <bool ANY, int OCC>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, 8))) void k_query_quad(RtSceneView S, const float4_* __restrict__ rays,
                                                     float* __restrict__ out_t, int* __restrict__ out_k, int n)
 {
     __shared__ uint32_t s_lds[2 * RT_QSTACK * 64];
@@ -1327,8 +1327,10 @@ extern "C" int rt_device_queries(rt_context* c, int mode, const float* rays, int
             case 1: hipLaunchKernelGGL((k_query<true, 0>), dim3(blocks), dim3(threads), 0, 0, b->view, d_rays, d_t, d_k, n, sr, sk); break;
             case 2: hipLaunchKernelGGL((k_query<false, 1>), dim3(blocks), dim3(threads), 0, 0, b->view, d_rays, d_t, d_k, n, sr, sk); break;
             case 3: hipLaunchKernelGGL((k_query<true, 1>), dim3(blocks), dim3(threads), 0, 0, b->view, d_rays, d_t, d_k, n, sr, sk); break;
-            case 4: hipLaunchKernelGGL((k_query_quad<false>), dim3(qblocks), dim3(threads), 0, 0, b->view, d_rays, d_t, d_k, n); break;
-            default: hipLaunchKernelGGL((k_query_quad<true>), dim3(qblocks), dim3(threads), 0, 0, b->view, d_rays, d_t, d_k, n); break;
+            case 4: hipLaunchKernelGGL((k_query_quad<false, 1>), dim3(qblocks), dim3(threads), 0, 0, b->view, d_rays, d_t, d_k, n); break;
+            case 5: hipLaunchKernelGGL((k_query_quad<true, 1>), dim3(qblocks), dim3(threads), 0, 0, b->view, d_rays, d_t, d_k, n); break;
+            case 6: hipLaunchKernelGGL((k_query_quad<false, 8>), dim3(qblocks), dim3(threads), 0, 0, b->view, d_rays, d_t, d_k, n); break;
+            default: hipLaunchKernelGGL((k_query_quad<true, 8>), dim3(qblocks), dim3(threads), 0, 0, b->view, d_rays, d_t, d_k, n); break;
         }
     };
     launch();  // warm-up

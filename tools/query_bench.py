@@ -55,7 +55,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, default=1 << 20)
     ap.add_argument("--reps", type=int, default=5)
-    ap.add_argument("--modes", default="0,2,4,1,3,5")
+    ap.add_argument("--modes", default="0,2,4,6,1,3,5,7")
     args = ap.parse_args()
     import bench
     import rt_amd
@@ -69,7 +69,7 @@ def main():
     L = _capi.lib()
     res = {}
     names = {0: "closest/node-walk", 1: "any/node-walk", 2: "closest/item-walk", 3: "any/item-walk",
-             4: "closest/quad-walk", 5: "any/quad-walk"}
+             4: "closest/quad-walk", 5: "any/quad-walk", 6: "closest/quad-walk@8w", 7: "any/quad-walk@8w"}
     for m in [int(x) for x in args.modes.split(",")]:
         t = np.zeros(args.n, dtype=np.float32)
         k = np.zeros(args.n, dtype=np.int32)
@@ -83,7 +83,7 @@ def main():
                 "fallback": fb, "hits": int((t > 0).sum())}
         print(json.dumps(line), flush=True)
     # agreement between walks
-    for a, b in ((0, 2), (1, 3), (0, 4), (1, 5)):
+    for a, b in ((0, 2), (1, 3), (0, 4), (1, 5), (0, 6), (1, 7)):
         if a in res and b in res:
             ta, ka = res[a]
             tb, kb = res[b]
