@@ -221,13 +221,17 @@ __device__ __forceinline__ void shard_prefix(const int32_t* cnt, int m, AT at, i
         pre[g * 64 + lane_id() + 1] = v;
     }
     __syncthreads();
-    if (threadIdx.x == 0) {  // chain the groups
-        pre[0] = 0;
-        for (int g = 1; g < m / 64; g++) {
-            const int off = pre[g * 64];
-            for (int j = 1; j <= 64; j++) pre[g * 64 + j] += off;
-        }
+    // chain the groups: entry (g, lane) adds the totals of groups < g (read before any write)
+    int add[8];
+    const int ng = m / 64;
+    for (int g = w; g < ng && g < 8 * nw; g += nw) {
+        int off = 0;
+        for (int h = 0; h < g; h++) off += pre[h * 64 + 64];
+        add[g / nw] = off;
     }
+    __syncthreads();
+    for (int g = w; g < ng && g < 8 * nw; g += nw) pre[g * 64 + lane_id() + 1] += add[g / nw];
+    if (threadIdx.x == 0) pre[0] = 0;
     __syncthreads();
 }
 
@@ -946,6 +950,7 @@ struct WaveLane {
     hipStream_t s = nullptr;
     hipEvent_t ev = nullptr;
     int n = 0, it = 0, tail_iter = -1;
+    long live = 0;  // live paths at the last readback (an upper bound: paths only finish)
     bool done = false, tail_next = false;
     int await = 0;  // 0 none, 1 live count, 2 fallback counts (tail entry check)
     hipEvent_t (*tev)[RT_MAX_TIMED_ITERS] = nullptr;  // [3][RT_MAX_TIMED_ITERS]
@@ -1002,6 +1007,7 @@ static int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounce
             lfb = fb + (size_t)l * src.W;
             fb_rs = nl;
         }
+        La.live = La.n;
         La.s = l == 0 ? s : b->ls[l];
         La.cnt = (int32_t*)b->counters[l].p;
         La.h = b->h_act[l];
@@ -1050,7 +1056,16 @@ static int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounce
     // guards against a runaway loop.
     const long max_iters = 64l * spp * ((long)bounces + 1) + 4096;
     const size_t act_bytes = RT_QSHARDS * RT_CSTRIDE * 4;
-    auto step_blocks_of = [&](const WaveLane& La) { return std::min((La.n + threads - 1) / threads, dev_cus * 8); };
+    // grids sized by the last known live count: k_step one slot per thread; k_trace up to
+    // five queries per path, a quad each, over two grid-fills, never fewer blocks than the
+    // exact-walk roles can claim (dev_cus * 4) plus room for the fast roles
+    auto step_blocks_of = [&](const WaveLane& La) {
+        return (int)std::max(1l, std::min((La.live + threads - 1) / threads, (long)dev_cus * 8));
+    };
+    auto trace_blocks_of = [&](const WaveLane& La) {
+        const long want = (20 * La.live + 2 * threads - 1) / (2 * threads);
+        return (int)std::min((long)trace_blocks, std::max(want, (long)dev_cus * 4 + 64));
+    };
     auto launch_trace = [&](WaveLane& La) -> int {
         rtk::WaveView& W = La.W;
         const int par = La.it & 1;
@@ -1063,9 +1078,9 @@ static int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounce
                 if (!La.tev[k][La.it]) HIPCHK(c, hipEventCreate(&La.tev[k][La.it]));
         if (T) HIPCHK(c, hipEventRecord(La.tev[0][La.it], La.s));
         if (S)
-            hipLaunchKernelGGL(k_trace<true>, dim3(trace_blocks), dim3(threads), 0, La.s, W, par, stats);
+            hipLaunchKernelGGL(k_trace<true>, dim3(trace_blocks_of(La)), dim3(threads), 0, La.s, W, par, stats);
         else
-            hipLaunchKernelGGL(k_trace<false>, dim3(trace_blocks), dim3(threads), 0, La.s, W, par, stats);
+            hipLaunchKernelGGL(k_trace<false>, dim3(trace_blocks_of(La)), dim3(threads), 0, La.s, W, par, stats);
         if (T) HIPCHK(c, hipEventRecord(La.tev[1][La.it], La.s));
         HIPCHK(c, hipGetLastError());
         return RT_OK;
@@ -1129,6 +1144,7 @@ static int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounce
         }
         long live = 0;
         for (int j = 0; j < RT_QSHARDS; j++) live += La.h[j * RT_CSTRIDE];
+        La.live = live;
         La.done = live == 0;
         La.tail_next = !La.done && live <= tail_max;
         return RT_OK;
