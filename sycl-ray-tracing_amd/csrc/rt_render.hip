@@ -612,8 +612,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_OC
 // walk, so every path is ready to step; a query the quad walk cannot answer
 // is answered here by the exact walk, inline, by lane 0 of its quad.
 #define RT_TAIL_MAXP 16  // paths per wave at most (5 rays each: 80 per list)
+#ifndef RT_TAIL_OCC
+#define RT_TAIL_OCC 3    // k_tail waves per SIMD (2: no spills but half the paths per launch; 3 measured faster)
+#endif
 template <bool STATS>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) void k_tail(rtk::WaveView W, int par, unsigned long long* stats)
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TAIL_OCC, RT_TAIL_OCC))) void k_tail(rtk::WaveView W, int par, unsigned long long* stats)
 {
     __shared__ rtk::RayRec s_q[4][2][RT_TAIL_MAXP * rtk::RK_COUNT];  // per wave: closest list, occlusion list
     __shared__ uint32_t s_stk[2 * RT_QSTACK * 64];
@@ -982,7 +985,7 @@ static int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounce
     WaveLane L[RT_MAX_LANES];
     int tail_p = 4;
     if (const char* e = getenv("RT_TAIL_PATHS")) tail_p = std::min(RT_TAIL_MAXP, std::max(0, atoi(e)));
-    const int tail_blocks = dev_cus * 3;  // k_tail holds path_step's registers: 3 waves per SIMD
+    const int tail_blocks = dev_cus * RT_TAIL_OCC;  // one grid-fill of k_tail
     const long tail_max = (long)tail_blocks * 4 * tail_p / nl;
     if (nl > 1) {
         HIPCHK(c, hipEventRecord(b->ev_fork, s));
