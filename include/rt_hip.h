@@ -98,6 +98,13 @@ int rt_render_pixels(rt_context* ctx, int width, int height, int samples, int ma
  * normal[3], u, v} with u = v = -1 (unused downstream). */
 int rt_intersect(rt_context* ctx, const float* rays, int n, void* out);
 
+/* USE_BVH (render_kernel.h:13, render_kernel.cpp:504-511): 1 (the reference's
+ * build, the default) answers INTERSECT_SCENE with the octree walk
+ * (intersect_scene_bvh :485-502); 0 with the brute-force triangle loop
+ * (intersect_scene :453-483: closest by strict `<` in buffer order, so the
+ * lowest triangle index wins a tie). */
+int rt_set_intersect_mode(rt_context* ctx, int use_bvh);
+
 /* Counters of the last render when enabled (RT_STAT_* order, rt_device.h);
  * with n up to 2 * RT_STAT_COUNT the second block is the share of the
  * gfx950 tail kernel (k_tail) in those totals. */

@@ -334,6 +334,7 @@ struct Scene {
     int ew = 0, eh = 0;
     std::vector<Col> env;
     std::vector<float> env_lum, cdf;
+    bool brute = false;  // INTERSECT_SCENE with USE_BVH 0 (render_kernel.h:13, render_kernel.cpp:504-511)
     ~Scene() { delete root; }
 };
 
@@ -348,8 +349,29 @@ bool bvh_intersect(const Scene& S, const Ray& ray, Hit& hit, Counters* cnt)  // 
     return S.root->intersect(S.tris, ray, hit, trash, den, num, cnt);
 }
 
+// RenderKernel::intersect_scene, the brute-force loop (render_kernel.cpp:453-483)
+bool intersect_scene_brute(const Scene& S, const Ray& ray, Hit& closest)
+{
+    closest.t = -1.0f;
+    for (int i = 0; i < (int)S.tris.size(); i++) {
+        Hit h;
+        if (tri_intersect(S.tris[i], ray, h))
+            if (h.t < closest.t || closest.t == -1.0f) {
+                closest = h;
+                closest.prim = i;
+            }
+    }
+    for (const Sph& sp : S.sph) {
+        Hit lh;
+        if (sph_intersect(sp, ray, lh))
+            if (lh.t < closest.t || closest.t == -1.0f) closest = lh;
+    }
+    return closest.t > 0.0f;
+}
+
 bool intersect_scene(const Scene& S, const Ray& ray, Hit& h, Counters* cnt)  // render_kernel.cpp:485-502
 {
+    if (S.brute) return intersect_scene_brute(S, ray, h);
     bvh_intersect(S, ray, h, cnt);
     for (const Sph& sp : S.sph) {
         Hit lh;
@@ -758,6 +780,9 @@ void* oracle_scene_create(const float* tris, int ntri, const int* mat_idx, const
 }
 
 void oracle_scene_destroy(void* s) { delete (Scene*)s; }
+
+// USE_BVH (render_kernel.h:13): 1 = octree (the reference's build), 0 = brute-force loop
+void oracle_set_use_bvh(void* s, int use_bvh) { ((Scene*)s)->brute = use_bvh == 0; }
 
 // Pre-order dump of the octree: per node {leaf, ntris, tris..., 6 floats min/max, 14 floats planes},
 // the same record format as oracle/ref/ref_driver.cpp "bvh". Returns bytes written (or needed).

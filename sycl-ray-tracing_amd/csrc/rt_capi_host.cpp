@@ -37,6 +37,7 @@ RtSceneView rt_host_view(const rt_context* c)
     v.env = c->env.data();
     v.env_lum = c->env_lum.data();
     v.cdf = c->cdf.data();
+    v.brute = c->brute ? 1 : 0;
     v.cdf_row = c->cdf_row.data();
     v.cdf_fence = c->cdf_fence.empty() ? nullptr : c->cdf_fence.data();
     v.cdf_coarse = c->cdf_coarse.data();
@@ -290,6 +291,14 @@ int rt_intersect(rt_context* c, const float* rays, int n, void* out)
         c->dirty = false;
     }
     return rt_backend_intersect(c, rays, n, out);
+}
+
+int rt_set_intersect_mode(rt_context* c, int use_bvh)
+{
+    if (!c) return RT_ERR_ARG;
+    c->brute = use_bvh == 0;
+    c->dirty = true;
+    return RT_OK;
 }
 
 int rt_set_stats(rt_context* c, int enabled)

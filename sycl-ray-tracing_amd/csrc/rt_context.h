@@ -39,6 +39,7 @@ struct rt_context {
     RtCamera cam{};
     bool have_cam = false;
 
+    bool brute = false;           // USE_BVH 0 (rt_set_intersect_mode)
     bool stats_enabled = false;
     unsigned long long stats[2 * RT_STAT_COUNT] = {};  // all kernels, then the gfx950 tail kernel's share
     double last_kernel_ms = 0.0;

@@ -80,7 +80,8 @@ struct RtSceneView {
     const float* cdf_coarse;  // [eh][cdf_cw]  cdf[y*ew + 32j + 31]
     const float* cdf_fence;   // [1 + eh][272] fence tables (rt_trace.h cdf_search_fence), or null
     int32_t n_emissive, n_spheres, ew, eh;
-    int32_t n_tris, chain_monotone, cdf_cw, pad2;  // chain_monotone: see rt_fast.h chain_ok
+    int32_t n_tris, chain_monotone, cdf_cw;  // chain_monotone: see rt_fast.h chain_ok
+    int32_t brute;  // 1: INTERSECT_SCENE is the brute-force loop (USE_BVH 0, render_kernel.cpp:453-483)
     // search BVH + octree back-links for the verification walk
     const Bvh4Node* bvh4;      // [0] = root
     const float4_* bvh_tri4;   // 3 records per triangle in BVH leaf order: {a.xyz, k}, {e1, leaf record}, {e2}

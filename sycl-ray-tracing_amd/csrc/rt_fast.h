@@ -154,7 +154,33 @@ struct FastHit {
     int leaf;     // its octree leaf record
     bool tie;     // another triangle hit at exactly t
     bool ovf;     // the bounded stack overflowed: answer unknown
+    int prim;     // brute-force mode: original index of t's triangle, the lowest among the ties
 };
+
+// One M-T hit (t, leaf-order k, octree leaf, original index prim) into h:
+// closest, tie flag, second-closest; in brute-force mode (USE_BVH 0) a tie
+// goes to the lowest original index, as the reference's strict `<` loop does.
+RT_HD void fast_take(FastHit& h, float t, int k, int leaf, int prim, bool brute)
+{
+    if (t < h.t) {
+        h.t2 = h.t;
+        h.t = t;
+        h.k = k;
+        h.leaf = leaf;
+        h.prim = prim;
+        h.tie = false;
+    } else if (t == h.t) {
+        h.tie = true;
+        h.t2 = t;
+        if (brute && prim < h.prim) {
+            h.k = k;
+            h.leaf = leaf;
+            h.prim = prim;
+        }
+    } else if (t < h.t2) {
+        h.t2 = t;
+    }
+}
 
 RT_HD void fast_leaf(const RtSceneView& S, int first, int count, V3 o, V3 d, FastHit& h, Stats* st)
 {
@@ -164,20 +190,8 @@ RT_HD void fast_leaf(const RtSceneView& S, int first, int count, V3 o, V3 d, Fas
     for (int j = 0; j < 4; j++) {
         if (j >= count) break;
         float t;
-        if (tri_test_v(ld3(L.a[j]), ld3(L.e1[j]), ld3(L.e2[j]), o, d, t)) {
-            if (t < h.t) {
-                h.t2 = h.t;
-                h.t = t;
-                h.k = (int)rt_asuint(L.a[j].w);
-                h.leaf = (int)rt_asuint(L.e1[j].w);
-                h.tie = false;
-            } else if (t == h.t) {
-                h.tie = true;
-                h.t2 = t;
-            } else if (t < h.t2) {
-                h.t2 = t;
-            }
-        }
+        if (tri_test_v(ld3(L.a[j]), ld3(L.e1[j]), ld3(L.e2[j]), o, d, t))
+            fast_take(h, t, (int)rt_asuint(L.a[j].w), (int)rt_asuint(L.e1[j].w), (int)rt_asuint(L.e2[j].w), S.brute != 0);
     }
     if (st) st->c[RT_STAT_TRI] += count;
 }
@@ -194,6 +208,7 @@ RT_HD void fast_closest(const RtSceneView& S, V3 o, V3 d, STK& stk, FastHit& h, 
     h.t = __builtin_inff();
     h.t2 = __builtin_inff();
     h.k = -1;
+    h.prim = 0x7fffffff;
     h.tie = false;
     h.ovf = false;
     if (st) st->c[RT_STAT_RAYS]++;
@@ -314,6 +329,7 @@ RT_HD void fast_closest_u(const RtSceneView& S, V3 o, V3 d, STK& stk, FastHit& h
     h.t = __builtin_inff();
     h.t2 = __builtin_inff();
     h.k = -1;
+    h.prim = 0x7fffffff;
     h.tie = false;
     h.ovf = false;
     if (st) st->c[RT_STAT_RAYS]++;
@@ -375,20 +391,9 @@ RT_HD void fast_closest_u(const RtSceneView& S, V3 o, V3 d, STK& stk, FastHit& h
             for (int j = 0; j < 4; j++) {
                 if (j >= cnt) break;
                 float t;
-                if (tri_test_v(ld3(R.q[3 * j]), ld3(R.q[3 * j + 1]), ld3(R.q[3 * j + 2]), o, d, t)) {
-                    if (t < h.t) {
-                        h.t2 = h.t;
-                        h.t = t;
-                        h.k = (int)rt_asuint(R.q[3 * j].w);
-                        h.leaf = (int)rt_asuint(R.q[3 * j + 1].w);
-                        h.tie = false;
-                    } else if (t == h.t) {
-                        h.tie = true;
-                        h.t2 = t;
-                    } else if (t < h.t2) {
-                        h.t2 = t;
-                    }
-                }
+                if (tri_test_v(ld3(R.q[3 * j]), ld3(R.q[3 * j + 1]), ld3(R.q[3 * j + 2]), o, d, t))
+                    fast_take(h, t, (int)rt_asuint(R.q[3 * j].w), (int)rt_asuint(R.q[3 * j + 1].w),
+                              (int)rt_asuint(R.q[3 * j + 2].w), S.brute != 0);
             }
         }
         // pop, dropping entries the window has closed behind
@@ -450,6 +455,7 @@ RT_HD int fast_any_u(const RtSceneView& S, V3 o, V3 d, STK& stk, Stats* st)
                 if (j >= cnt) break;
                 float t;
                 if (tri_test_v(ld3(R.q[3 * j]), ld3(R.q[3 * j + 1]), ld3(R.q[3 * j + 2]), o, d, t)) {
+                    if (S.brute) return 1;  // USE_BVH 0: any triangle hit occludes
                     if (!kset) {
                         ray_setup(o, d, K);
                         kset = true;
@@ -478,6 +484,11 @@ RT_HD bool fast_query_closest(const RtSceneView& S, V3 o, V3 d, STK& stk, float&
     if (h.k < 0) {  // no M-T hit anywhere: the reference finds none either
         t_out = -1.0f;
         k_out = -1;
+        return true;
+    }
+    if (S.brute) {  // USE_BVH 0: the closest M-T hit, lowest index on ties; no octree
+        t_out = h.t;
+        k_out = h.k;
         return true;
     }
     if (h.tie) return false;
@@ -522,6 +533,7 @@ RT_HD int fast_query_any(const RtSceneView& S, V3 o, V3 d, STK& stk, Stats* st)
                 if (j >= cnt) break;
                 float t;
                 if (tri_test_v(ld3(L.a[j]), ld3(L.e1[j]), ld3(L.e2[j]), o, d, t)) {
+                    if (S.brute) return 1;  // USE_BVH 0: any triangle hit occludes
                     if (!kset) {
                         ray_setup(o, d, K);
                         kset = true;

@@ -149,7 +149,7 @@ static int run_wave_host(rt_context* c, int w, int h, int spp, int bounces, cons
                     if (ps) ps->c[RT_STAT_FALLBACK]++;
                     has = rtk::trava_begin(W.S, T, rtk::v3of(r.o), rtk::v3of(r.d), ps);
                     if (!has) {
-                        rtk::finish_any(W, target, false);
+                        rtk::finish_any(W, target, T.hit);  // (false, or the brute-force answer)
                         __atomic_fetch_sub(&W.r_park[target >> 3], 1, __ATOMIC_RELAXED);
                     }
                 }

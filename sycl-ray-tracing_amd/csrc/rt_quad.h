@@ -92,13 +92,15 @@ __device__ __forceinline__ QChild quad_child(const RtSceneView& S, int node, int
 
 // Lane `sub`'s triangle of a leaf item: Moller-Trumbore (the reference's
 // arithmetic). Returns t (+inf when the lane has no triangle or no hit).
-__device__ __forceinline__ float quad_tri(const RtSceneView& S, int item, int sub, V3 o, V3 d, int& k, int& leaf)
+__device__ __forceinline__ float quad_tri(const RtSceneView& S, int item, int sub, V3 o, V3 d, int& k, int& leaf,
+                                          int& prim)
 {
     const int v = ~item;
     const int first = v >> 2, cnt = (v & 3) + 1;
     float tv = __builtin_inff();
     k = -1;
     leaf = -1;
+    prim = 0x7fffffff;
     if (sub < cnt) {
         const float4_* p = S.bvh_tri4 + 3 * (first + sub);
         const float4_ a = p[0], e1 = p[1], e2 = p[2];
@@ -107,6 +109,7 @@ __device__ __forceinline__ float quad_tri(const RtSceneView& S, int item, int su
             tv = t;
             k = (int)rt_asuint(a.w);
             leaf = (int)rt_asuint(e1.w);
+            prim = (int)rt_asuint(e2.w);
         }
     }
     return tv;
@@ -120,6 +123,7 @@ __device__ void quad_closest(const RtSceneView& S, V3 o, V3 d, QSTK& stk, int su
     h.t2 = __builtin_inff();
     h.k = -1;
     h.leaf = -1;
+    h.prim = 0x7fffffff;
     h.tie = false;
     h.ovf = false;
     if (st && sub == 0) st->c[RT_STAT_RAYS]++;
@@ -155,8 +159,8 @@ __device__ void quad_closest(const RtSceneView& S, V3 o, V3 d, QSTK& stk, int su
             }
         } else {
             if (st && sub == 0) st->c[RT_STAT_TRI] += ((~cur) & 3) + 1;
-            int k, leaf;
-            const float tv = quad_tri(S, cur, sub, o, d, k, leaf);
+            int k, leaf, prim;
+            const float tv = quad_tri(S, cur, sub, o, d, k, leaf, prim);
             // quad (smallest, second smallest) of the lanes' hit distances
             float m1 = tv, m2 = __builtin_inff();
             {
@@ -169,18 +173,27 @@ __device__ void quad_closest(const RtSceneView& S, V3 o, V3 d, QSTK& stk, int su
                 const float n1 = __builtin_fminf(m1, o1), n2 = __builtin_fminf(__builtin_fmaxf(m1, o1), __builtin_fminf(m2, o2));
                 m1 = n1, m2 = n2;
             }
+            // the lane holding m1 with the lowest original index (brute-force mode: the reference's
+            // loop keeps the lowest index of a tie; octree mode: any tie falls back anyway)
+            int pm = tv == m1 ? prim : 0x7fffffff;
+            pm = min(pm, qdpp<RT_QX1>(pm));
+            pm = min(pm, qdpp<RT_QX2>(pm));
+            const bool mine = tv == m1 && prim == pm;
             if (m1 < h.t) {
-                // the lowest lane holding m1 (a second one would make m2 == m1: a tie)
-                const bool mine = tv == m1 && !(qdppf<RT_QX1>(tv) == m1 && s_lower(sub, 1)) &&
-                                  !(qdppf<RT_QX2>(tv) == m1 && s_lower(sub, 2)) && !(qdppf<RT_QX3>(tv) == m1 && s_lower(sub, 3));
                 h.t2 = __builtin_fminf(h.t, m2);
                 h.t = m1;
                 h.k = qor(mine ? k : 0);
                 h.leaf = qor(mine ? leaf : 0);
+                h.prim = pm;
                 h.tie = m2 == m1;
             } else if (m1 == h.t && m1 < __builtin_inff()) {
                 h.tie = true;
                 h.t2 = m1;
+                if (pm < h.prim) {
+                    h.k = qor(mine ? k : 0);
+                    h.leaf = qor(mine ? leaf : 0);
+                    h.prim = pm;
+                }
             } else {
                 h.t2 = __builtin_fminf(h.t2, m1);
             }
@@ -212,6 +225,11 @@ __device__ bool quad_query_closest(const RtSceneView& S, V3 o, V3 d, QSTK& stk, 
     if (h.k < 0) {
         t_out = -1.0f;
         k_out = -1;
+        return true;
+    }
+    if (S.brute) {  // USE_BVH 0: the closest M-T hit, lowest index on ties; no octree
+        t_out = h.t;
+        k_out = h.k;
         return true;
     }
     if (h.tie) return false;
@@ -257,10 +275,12 @@ __device__ int quad_query_any(const RtSceneView& S, V3 o, V3 d, QSTK& stk, int s
             }
         } else {
             if (st && sub == 0) st->c[RT_STAT_ANY_TRI] += ((~cur) & 3) + 1;
-            int k, leaf;
-            const float tv = quad_tri(S, cur, sub, o, d, k, leaf);
+            int k, leaf, prim;
+            const float tv = quad_tri(S, cur, sub, o, d, k, leaf, prim);
             int hit = 0;
-            if (tv < __builtin_inff()) {
+            if (tv < __builtin_inff() && S.brute) {
+                hit = 1;  // USE_BVH 0: any triangle hit occludes
+            } else if (tv < __builtin_inff()) {
                 RayK K;
                 ray_setup(o, d, K);
                 hit = chain_ok(S, K, leaf, false, 0.0f, st) ? 1 : 0;

@@ -440,7 +440,7 @@ __device__ void exact_any(const rtk::WaveView& W, int par, uint32_t* lds, int la
                     if (st) st->c[RT_STAT_FALLBACK]++;
                     has = rtk::trava_begin(W.S, T, rtk::v3of(r.o), rtk::v3of(r.d), st);
                     if (!has) {
-                        rtk::finish_any(W, target, false);
+                        rtk::finish_any(W, target, T.hit);  // (false, or the brute-force answer)
                         atomicSub(&W.r_park[target >> 3], 1);
                     }
                 }
@@ -708,13 +708,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TAIL_OCC
                             rtk::finish_closest(W, target, T.o, T.d, T.best_t, T.best_k);
                         } else {
                             rtk::TravA T;
-                            bool hit = false;
-                            if (rtk::trava_begin(W.S, T, o, d, ps)) {
+                            if (rtk::trava_begin(W.S, T, o, d, ps))
                                 while (rtk::trava_step(W.S, T, xs, ps)) {
                                 }
-                                hit = T.hit;
-                            }
-                            rtk::finish_any(W, target, hit);
+                            rtk::finish_any(W, target, T.hit);  // (begin leaves the brute-force answer in T.hit)
                         }
                     }
                 }
@@ -931,6 +928,7 @@ int rt_backend_upload(rt_context* c)
     v.eh = c->eh;
     v.n_tris = (int)(c->tris.size() / 9);
     v.chain_monotone = c->flat.chain_monotone ? 1 : 0;
+    v.brute = c->brute ? 1 : 0;
     v.bvh4 = (const Bvh4Node*)b->bvh4.p;
     v.bvh_tri4 = (const float4_*)b->bvh_tri4.p;
     v.parent = (const int32_t*)b->parent.p;

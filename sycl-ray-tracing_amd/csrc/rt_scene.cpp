@@ -751,6 +751,7 @@ void build_search_bvh(FlatBvh& out)
         out.bvh_tri4[3 * (size_t)i + 1] = out.tri4[3 * (size_t)k + 1];
         std::memcpy(&out.bvh_tri4[3 * (size_t)i + 1].w, &out.leaf_of[k], 4);  // octree leaf record
         out.bvh_tri4[3 * (size_t)i + 2] = out.tri4[3 * (size_t)k + 2];
+        out.bvh_tri4[3 * (size_t)i + 2].w = out.tri4[3 * (size_t)k].w;  // original triangle index (brute-force ties)
     }
     if (out.bvh.empty()) {  // no triangles: a root with two empty slots
         BvhNode r{};

@@ -217,6 +217,33 @@ RT_HD bool tri_test(const float4_* tri4, int k, V3 o, V3 d, float& t_out)
     return tri_test_v(ld3(tri4[3 * k]), ld3(tri4[3 * k + 1]), ld3(tri4[3 * k + 2]), o, d, t_out);
 }
 
+// RenderKernel::intersect_scene, the brute-force triangle loop (USE_BVH 0,
+// render_kernel.cpp:453-471): every triangle in buffer order, the closest kept
+// with a strict `<`, so the lowest index wins a tie. Returns the leaf-order
+// index k (-1: none) and t (-1: none); the sphere loop follows (rt_wave.h).
+RT_HD void brute_closest(const RtSceneView& S, V3 o, V3 d, float& best_t, int& best_k)
+{
+    best_t = -1.0f;
+    best_k = -1;
+    for (int i = 0; i < S.n_tris; i++) {
+        const int k = S.prim2k[i];
+        float t;
+        if (tri_test(S.tri4, k, o, d, t))
+            if (t < best_t || best_t == -1.0f) {
+                best_t = t;
+                best_k = k;
+            }
+    }
+}
+RT_HD bool brute_any(const RtSceneView& S, V3 o, V3 d)  // INTERSECT_SCENE as a boolean
+{
+    for (int i = 0; i < S.n_tris; i++) {
+        float t;
+        if (tri_test(S.tri4, i, o, d, t) && t > 0.0f) return true;
+    }
+    return false;
+}
+
 // ------------------------------------------------ libstdc++ heap emulation
 // std::priority_queue<QueueElement, vector, greater> (bvh.h:170-199): pushes
 // in child order, pops the minimum t_near. Equal keys pop in the order

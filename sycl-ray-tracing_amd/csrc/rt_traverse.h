@@ -133,6 +133,10 @@ RT_HD bool travc_begin(const RtSceneView& S, TravC& T, V3 o, V3 d, Stats* st)
     T.steps = 0;
     T.mode = TM_DONE;
     if (st) st->c[RT_STAT_RAYS]++;
+    if (S.brute) {  // USE_BVH 0: the loop answers at once
+        brute_closest(S, o, d, T.best_t, T.best_k);
+        return false;
+    }
     if (!ray_setup(o, d, T.K)) return false;
     float tn;
     if (st) st->c[RT_STAT_VOL]++;
@@ -320,6 +324,10 @@ RT_HD bool trava_begin(const RtSceneView& S, TravA& T, V3 o, V3 d, Stats* st)
     T.hit = false;
     T.mode = TM_DONE;
     if (st) st->c[RT_STAT_ANY_RAYS]++;
+    if (S.brute) {  // USE_BVH 0
+        T.hit = brute_any(S, o, d);
+        return false;
+    }
     if (!ray_setup(o, d, T.K)) return false;
     float tn;
     if (st) st->c[RT_STAT_ANY_VOL]++;

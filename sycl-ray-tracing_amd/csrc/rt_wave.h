@@ -591,7 +591,10 @@ RT_HD void spheres_closest(const RtSceneView& S, V3 o, V3 d, float& t, int& k)
 
 RT_HD void query_closest(const RtSceneView& S, V3 o, V3 d, StackEnt* stack, float& t, int& k, Stats* st)
 {
-    trace_closest(S, o, d, stack, t, k, st);
+    if (S.brute)
+        brute_closest(S, o, d, t, k);
+    else
+        trace_closest(S, o, d, stack, t, k, st);
     spheres_closest(S, o, d, t, k);
 }
 

@@ -258,6 +258,11 @@ class RenderKernel:
         check(self.L, self.L.rt_intersect(self.ctx, ptr(rays), rays.shape[0], ptr(out)), self.ctx, "rt_intersect")
         return out
 
+    def set_use_bvh(self, use_bvh: bool = True):
+        """USE_BVH (render_kernel.h:13): False switches INTERSECT_SCENE to the
+        brute-force intersect_scene loop (render_kernel.cpp:453-483)."""
+        check(self.L, self.L.rt_set_intersect_mode(self.ctx, 1 if use_bvh else 0), self.ctx, "rt_set_intersect_mode")
+
     def set_stats(self, on: bool):
         self.L.rt_set_stats(self.ctx, 1 if on else 0)
 

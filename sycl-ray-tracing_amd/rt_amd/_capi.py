@@ -23,6 +23,7 @@ EXPORTS = [
     "rt_render_device", "rt_render_pixels", "rt_intersect", "rt_set_stats", "rt_get_stats", "rt_last_kernel_ms",
     "rt_mesh_load", "rt_mesh_counts", "rt_mesh_copy", "rt_mesh_free", "rt_camera_preset", "rt_env_luminance_cdf",
     "rt_octree_dump", "rt_read_hdr", "rt_write_png", "rt_image_to_rgba8",
+    "rt_set_intersect_mode",
 ]
 
 P = ctypes.c_void_p
@@ -47,6 +48,7 @@ _SIGS = {
     "rt_render_pixels": (I, [P, I, I, I, I, P, I, P]),
     "rt_intersect": (I, [P, P, I, P]),
     "rt_set_stats": (I, [P, I]),
+    "rt_set_intersect_mode": (I, [P, I]),
     "rt_get_stats": (I, [P, P, I]),
     "rt_last_kernel_ms": (ctypes.c_double, [P]),
     "rt_mesh_load": (I, [ctypes.c_char_p, ctypes.POINTER(P)]),

@@ -30,6 +30,7 @@ def lib():
         L.oracle_scene_create.argtypes = [P, ctypes.c_int, P, P, ctypes.c_int, P, ctypes.c_int, P, ctypes.c_int,
                                           P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]
         L.oracle_scene_destroy.argtypes = [P]
+        L.oracle_set_use_bvh.argtypes = [P, ctypes.c_int]
         L.oracle_bvh_dump.restype = ctypes.c_long
         L.oracle_bvh_dump.argtypes = [P, P, ctypes.c_long]
         L.oracle_intersect.argtypes = [P, P, ctypes.c_int, P, P]
@@ -68,6 +69,10 @@ class OracleScene:
         if getattr(self, "h", None):
             lib().oracle_scene_destroy(self.h)
             self.h = None
+
+    def set_use_bvh(self, use_bvh: bool):
+        """USE_BVH (render_kernel.h:13): False = the brute-force intersect_scene loop."""
+        lib().oracle_set_use_bvh(self.h, 1 if use_bvh else 0)
 
     def octree_dump(self) -> bytes:
         n = lib().oracle_bvh_dump(self.h, None, 0)
