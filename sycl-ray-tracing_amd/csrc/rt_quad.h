@@ -213,6 +213,58 @@ __device__ void quad_closest(const RtSceneView& S, V3 o, V3 d, QSTK& stk, int su
     if (h.k < 0) h.t = -1.0f;
 }
 
+// chain_ok (rt_fast.h) by a quad: lane j evaluates slab planes j and j + 4
+// (the last lane only plane 3) with ray_setup's and slab_test's arithmetic,
+// and the quad combines the running max / min. The reference's max / min
+// (`(a < b) ? b : a`) never let a NaN quotient into the accumulator, which
+// starts at -inf / +inf, so the combination order does not change the result
+// (a +-0 can differ in sign, and only ever meets comparisons). rec is
+// quad-uniform; the answer is returned to every lane.
+__device__ __forceinline__ bool quad_chain_ok(const RtSceneView& S, V3 o, V3 d, int rec, bool need_t2, float t2,
+                                              int sub, Stats* st)
+{
+    const float s3 = rt_sqrtf(3.0f) / 3;
+    // the 7 plane normals of bvh.cpp:8-16 (ray_setup), selected without a private array
+    auto normal = [&](int p) {
+        if (p < 3) return v3(p == 0 ? 1.0f : 0.0f, p == 1 ? 1.0f : 0.0f, p == 2 ? 1.0f : 0.0f);
+        return v3(p == 4 || p == 5 ? -s3 : s3, p == 5 || p == 6 ? -s3 : s3, s3);
+    };
+    const int p0 = sub, p1 = sub + 4;  // p1 == 7: none
+    const V3 n0 = normal(p0), n1 = normal(p1 < 7 ? p1 : 0);
+    const float num0 = dot(n0, o), num1 = dot(n1, o);
+    const double r0 = 1.0 / (double)dot(n0, d), r1 = 1.0 / (double)dot(n1, d);
+    for (;;) {
+        if (st && sub == 0) st->c[RT_STAT_VERIFY]++;
+        const float* nd = (const float*)(S.nodes + rec);  // RtNode: dn[7], df[7], ref, cnt
+        const float dn0 = nd[p0], df0 = nd[7 + p0], dn1 = nd[p1 < 7 ? p1 : 0], df1 = nd[7 + (p1 < 7 ? p1 : 0)];
+        float tn = -__builtin_inff(), tf = __builtin_inff();
+        {
+            const bool neg = r0 < 0.0;
+            float a = slab_div((neg ? df0 : dn0) - num0, r0), b = slab_div((neg ? dn0 : df0) - num0, r0);
+            if (__builtin_isinf(r0)) a = -__builtin_inff(), b = __builtin_inff();
+            tn = rt_max(tn, a);
+            tf = rt_min(tf, b);
+        }
+        if (p1 < 7) {
+            const bool neg = r1 < 0.0;
+            float a = slab_div((neg ? df1 : dn1) - num1, r1), b = slab_div((neg ? dn1 : df1) - num1, r1);
+            if (__builtin_isinf(r1)) a = -__builtin_inff(), b = __builtin_inff();
+            tn = rt_max(tn, a);
+            tf = rt_min(tf, b);
+        }
+        tn = rt_max(tn, qdppf<RT_QX1>(tn));
+        tn = rt_max(tn, qdppf<RT_QX2>(tn));
+        tf = rt_min(tf, qdppf<RT_QX1>(tf));
+        tf = rt_min(tf, qdppf<RT_QX2>(tf));
+        if (tf < tn) return false;
+        const int par = S.parent[rec];
+        if (par < 0) return true;
+        if (need_t2 && !(t2 >= tn)) return false;
+        if (S.chain_monotone) return true;
+        rec = par;
+    }
+}
+
 // fast_query_closest by a quad: true with (t, k) when answered, false when
 // the exact walk must answer (same cases as the one-lane walk).
 template <class QSTK>
@@ -233,15 +285,8 @@ __device__ bool quad_query_closest(const RtSceneView& S, V3 o, V3 d, QSTK& stk, 
         return true;
     }
     if (h.tie) return false;
-    // chain check on lane 0, broadcast
-    int ok = 0;
-    if (sub == 0) {
-        RayK K;
-        ray_setup(o, d, K);
-        const float t2 = __builtin_fminf(h.t2, h.t + h.t * RT_T2_WINDOW);
-        ok = chain_ok(S, K, h.leaf, true, t2, st) ? 1 : 0;
-    }
-    if (!qor(ok)) return false;
+    const float t2 = __builtin_fminf(h.t2, h.t + h.t * RT_T2_WINDOW);
+    if (!quad_chain_ok(S, o, d, h.leaf, true, t2, sub, st)) return false;
     t_out = h.t;
     k_out = h.k;
     return true;
@@ -277,15 +322,22 @@ __device__ int quad_query_any(const RtSceneView& S, V3 o, V3 d, QSTK& stk, int s
             if (st && sub == 0) st->c[RT_STAT_ANY_TRI] += ((~cur) & 3) + 1;
             int k, leaf, prim;
             const float tv = quad_tri(S, cur, sub, o, d, k, leaf, prim);
-            int hit = 0;
-            if (tv < __builtin_inff() && S.brute) {
-                hit = 1;  // USE_BVH 0: any triangle hit occludes
-            } else if (tv < __builtin_inff()) {
-                RayK K;
-                ray_setup(o, d, K);
-                hit = chain_ok(S, K, leaf, false, 0.0f, st) ? 1 : 0;
+            const int hitb = tv < __builtin_inff() ? 1 : 0;
+            if (S.brute) {
+                if (qor(hitb)) return 1;  // USE_BVH 0: any triangle hit occludes
+            } else {
+                // each hit lane's octree leaf in turn, checked by the whole quad
+                const int h1 = qdpp<RT_QX1>(hitb), h2 = qdpp<RT_QX2>(hitb), h3 = qdpp<RT_QX3>(hitb);
+                const int l1 = qdpp<RT_QX1>(leaf), l2 = qdpp<RT_QX2>(leaf), l3 = qdpp<RT_QX3>(leaf);
+#pragma unroll
+                for (int j = 0; j < 4; j++) {  // quad lane j (same order in every lane)
+                    const int x = j ^ sub;     // its distance in the xor pattern from this lane
+                    const int hj = x == 0 ? hitb : x == 1 ? h1 : x == 2 ? h2 : h3;
+                    if (!hj) continue;
+                    const int lj = x == 0 ? leaf : x == 1 ? l1 : x == 2 ? l2 : l3;
+                    if (quad_chain_ok(S, o, d, lj, false, 0.0f, sub, st)) return 1;
+                }
             }
-            if (qor(hit)) return 1;
         }
         if (have) continue;
         if (sp == 0) return 0;
