@@ -48,13 +48,17 @@ struct DevBuf {
 };
 
 // counters[] layout (int32). Iteration i (p = i & 1) runs k_trace(i) then
-// k_step(i); every set is zeroed by the launch before the one that fills it,
-// so no reset launch is needed:
+// k_step(i); every set is zeroed by a launch between its last reader and its
+// next writer, so no reset launch is needed:
 //   Q[p]      queue sizes     filled by k_step(i-1) / k_init, read by k_trace(i); k_trace(i) zeroes Q[p^1]
 //   ACT[p]    live count      filled by k_step(i-1) / k_init, read by k_step(i);  k_trace(i) zeroes ACT[p^1]
-//   FB[p]     fallback sizes  filled by k_trace(i-1), read by k_trace(i), which fills FB[p^1]; k_step(i) zeroes FB[p]
-//   PARK[p]   parked queries  likewise
-//   TK        exact-walk work tickets of k_trace(i); k_step(i) zeroes them
+//   FB[p]     fallback lists  filled by k_trace(i) (queries the quad walk could not settle), walked
+//                             exactly by k_step(i); k_step(i) zeroes FB[p^1] for k_trace(i + 1)
+//   PARK[p]   parked walks    filled by k_step(i), resumed by k_step(i + 1); k_trace(i) zeroes PARK[p]
+//   DONE[p]   finished walks  slots, filled by k_step(i); k_trace(i + 1) releases them (r_park -= 1)
+//                             and k_step(i + 1) zeroes DONE[p]. The release waits for a kernel
+//                             boundary so the walk's results are visible before the path steps.
+//   TK        exact-walk work tickets of k_step(i); k_trace(i) zeroes them
 //
 // Q and ACT are sharded: the appends of a 64-item input chunk go to one of
 // RT_QSHARDS shards (append_emit), each a segment of W.seg_cap entries with
@@ -73,6 +77,8 @@ enum {
     C_TK_EXACT_C,
     C_TK_EXACT_A,
     C_TK_TAIL,       // k_tail: next live-list entry to take
+    C_DONE0,
+    C_DONE1,
     C_SHARDED = 64,  // sharded counters from here (qc_at / ac_at)
 };
 #define RT_QSHARDS 64
@@ -260,38 +266,6 @@ __global__ __launch_bounds__(256) void k_init(rtk::WaveView W)
     append_emit(W, 0, p & ~63, W.n_slots, p, e);
 }
 
-template <bool STATS>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_STEP_OCC, 8))) void k_step(rtk::WaveView W, int par, unsigned long long* stats)
-{
-    __shared__ int s_pre[RT_QSHARDS + 1];
-    int32_t* cnt = W.counters;
-    if (blockIdx.x == 0 && threadIdx.x == 0) {  // read by k_trace(i); refilled by k_trace(i + 1)
-        cnt[C_FBC0 + par] = cnt[C_FBA0 + par] = cnt[C_PARKC0 + par] = cnt[C_PARKA0 + par] = 0;
-        cnt[C_TK_EXACT_C] = cnt[C_TK_EXACT_A] = 0;
-    }
-    shard_prefix(cnt, RT_QSHARDS, [&](int j) { return ac_at(par, j); }, s_pre);
-    const int n = s_pre[RT_QSHARDS];
-    if (STATS && W.iterq && blockIdx.x == 0 && threadIdx.x == 0 && W.iter < RT_MAX_TIMED_ITERS)
-        W.iterq[2 * W.iter + 1] = n;
-    rtk::Stats st;
-    if (STATS)
-        for (int i = 0; i < RT_STAT_COUNT; i++) st.c[i] = 0;
-    for (int base = wave_gid() * 64; base < n; base += wave_count() * 64) {
-        const int idx = base + lane_id();
-        rtk::Emit e;
-        e.mask = 0;
-        e.active = false;
-        int p = -1;
-        if (idx < n) {
-            const int sh = shard_find(s_pre, RT_QSHARDS, idx);
-            p = W.act_in[(size_t)sh * W.seg_cap + (idx - s_pre[sh])];
-            rtk::path_step(W, p, e, STATS ? &st : nullptr);
-        }
-        append_emit(W, par ^ 1, base, n, p, e);
-    }
-    flush_stats<STATS>(st, stats);
-}
-
 // ------------------------------------------------------------- query kernel
 // Every closest-hit and occlusion query of the iteration, plus the exact
 // octree walks of the queries the previous iteration could not settle, in
@@ -316,7 +290,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_STEP_OCC
 #define RT_REFILL 16
 #define RT_QSTACK 32            // quad walks (rt_quad.h): stack entries per quad (item + key, 64 quads per block)
 #ifndef RT_TRACE_OCC
-#define RT_TRACE_OCC 6          // k_trace blocks of 256 per CU (VGPR budget 512 / occupancy)
+#define RT_TRACE_OCC 6          // k_trace waves per SIMD (8 fits the quad walks in 64 VGPRs but measured
+                                // 512 vs 539 Msamples/s: more trace waves crowd the other lanes k_step)
 #endif
 
 // Search-BVH stack of a fast query: entries [0, N) in LDS (entry i of
@@ -353,6 +328,15 @@ __device__ __forceinline__ int split_blocks(int nb, int w0, int w1)
     return n0;
 }
 
+// A finished exact walk: its slot goes to DONE[par]; k_trace(i + 1) releases it.
+__device__ __forceinline__ void walk_done(const rtk::WaveView& W, int par, uint32_t target)
+{
+    const int j = atomicAdd(W.counters + C_DONE0 + par, 1);
+    W.done[par][j] = (int32_t)(target >> 3);
+}
+
+// Exact octree walks of k_step(i) (par = i & 1): the walks parked by k_step(i - 1)
+// (PARK[par ^ 1], the first n_res tickets), then the fallbacks of k_trace(i) (FB[par]).
 __device__ void exact_closest(const rtk::WaveView& W, int par, uint32_t* lds, int lane, int n_res, int total,
                               rtk::Stats* st)
 {
@@ -375,7 +359,7 @@ __device__ void exact_closest(const rtk::WaveView& W, int par, uint32_t* lds, in
             if (need) {
                 const int idx = base + __popcll(bneed & ((1ull << lane_id()) - 1ull));
                 if (idx < n_res) {
-                    target = rtk::travc_resume(&W.park_c[par][idx], T, stk);
+                    target = rtk::travc_resume(&W.park_c[par ^ 1][idx], T, stk);
                     has = true;
                 } else if (idx < total) {
                     const rtk::RayRec r = fb[idx - n_res];
@@ -384,7 +368,7 @@ __device__ void exact_closest(const rtk::WaveView& W, int par, uint32_t* lds, in
                     has = rtk::travc_begin(W.S, T, rtk::v3of(r.o), rtk::v3of(r.d), st);
                     if (!has) {
                         rtk::finish_closest(W, target, T.o, T.d, T.best_t, T.best_k);
-                        atomicSub(&W.r_park[target >> 3], 1);
+                        walk_done(W, par, target);
                     }
                 }
             }
@@ -396,12 +380,12 @@ __device__ void exact_closest(const rtk::WaveView& W, int par, uint32_t* lds, in
         if (has) {
             if (!rtk::travc_step(W.S, T, stk, st)) {
                 rtk::finish_closest(W, target, T.o, T.d, T.best_t, T.best_k);
-                atomicSub(&W.r_park[target >> 3], 1);
+                walk_done(W, par, target);
                 has = false;
             } else if (T.steps >= W.budget && rtk::travc_parkable(T)) {
-                const int ps = atomicAdd(W.counters + C_PARKC0 + (par ^ 1), 1);
+                const int ps = atomicAdd(W.counters + C_PARKC0 + par, 1);
                 if (ps < W.park_cap) {
-                    rtk::travc_park(T, stk, target, &W.park_c[par ^ 1][ps]);
+                    rtk::travc_park(T, stk, target, &W.park_c[par][ps]);
                     has = false;
                 } else {
                     T.steps = 0;  // park pool full: keep going
@@ -432,7 +416,7 @@ __device__ void exact_any(const rtk::WaveView& W, int par, uint32_t* lds, int la
             if (need) {
                 const int idx = base + __popcll(bneed & ((1ull << lane_id()) - 1ull));
                 if (idx < n_res) {
-                    target = rtk::trava_resume(&W.park_a[par][idx], T, stk);
+                    target = rtk::trava_resume(&W.park_a[par ^ 1][idx], T, stk);
                     has = true;
                 } else if (idx < total) {
                     const rtk::RayRec r = fb[idx - n_res];
@@ -441,7 +425,7 @@ __device__ void exact_any(const rtk::WaveView& W, int par, uint32_t* lds, int la
                     has = rtk::trava_begin(W.S, T, rtk::v3of(r.o), rtk::v3of(r.d), st);
                     if (!has) {
                         rtk::finish_any(W, target, T.hit);  // (false, or the brute-force answer)
-                        atomicSub(&W.r_park[target >> 3], 1);
+                        walk_done(W, par, target);
                     }
                 }
             }
@@ -453,12 +437,12 @@ __device__ void exact_any(const rtk::WaveView& W, int par, uint32_t* lds, int la
         if (has) {
             if (!rtk::trava_step(W.S, T, stk, st)) {
                 rtk::finish_any(W, target, T.hit);
-                atomicSub(&W.r_park[target >> 3], 1);
+                walk_done(W, par, target);
                 has = false;
             } else if (T.steps >= W.budget && rtk::trava_parkable(T)) {
-                const int ps = atomicAdd(W.counters + C_PARKA0 + (par ^ 1), 1);
+                const int ps = atomicAdd(W.counters + C_PARKA0 + par, 1);
                 if (ps < W.park_cap) {
-                    rtk::trava_park(T, stk, target, &W.park_a[par ^ 1][ps]);
+                    rtk::trava_park(T, stk, target, &W.park_a[par][ps]);
                     has = false;
                 } else {
                     T.steps = 0;
@@ -468,26 +452,30 @@ __device__ void exact_any(const rtk::WaveView& W, int par, uint32_t* lds, int la
     }
 }
 
+// Path step of iteration i (par = i & 1): resolve, shade, next sample, for
+// every live path not waiting on an exact walk; the first blocks instead run
+// the exact octree walks of this iteration's fallbacks and of the walks parked
+// last iteration (they need the registers this kernel has anyway; k_trace
+// stays small enough for 8 waves per SIMD).
 template <bool STATS>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_OCC, 8))) void k_trace(rtk::WaveView W, int par, unsigned long long* stats)
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_STEP_OCC, 8))) void k_step(rtk::WaveView W, int par, unsigned long long* stats)
 {
     __shared__ uint32_t s_lds[RT_LDS_WORDS * 256];
-    __shared__ int s_pre[rtk::RK_COUNT * RT_QSHARDS + 1];
+    __shared__ int s_pre[RT_QSHARDS + 1];
     int32_t* cnt = W.counters;
-    if (blockIdx.x == 0)  // filled by k_step(i) next
-        for (int j = threadIdx.x; j < (rtk::RK_COUNT + 1) * RT_QSHARDS; j += blockDim.x)
-            cnt[j < rtk::RK_COUNT * RT_QSHARDS ? qc_at(par ^ 1, j / RT_QSHARDS, j % RT_QSHARDS)
-                                                : ac_at(par ^ 1, j - rtk::RK_COUNT * RT_QSHARDS)] = 0;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {  // for k_trace(i + 1); DONE[par ^ 1] was released by k_trace(i)
+        cnt[C_FBC0 + (par ^ 1)] = cnt[C_FBA0 + (par ^ 1)] = 0;
+        cnt[C_DONE0 + (par ^ 1)] = 0;
+    }
     rtk::Stats st;
     if (STATS)
         for (int i = 0; i < RT_STAT_COUNT; i++) st.c[i] = 0;
     rtk::Stats* ps = STATS ? &st : nullptr;
-
-    // exact roles: 64 walks per block to start with (16 per wave), at most
-    // half of the spill lanes each
-    const int nrc = min(cnt[C_PARKC0 + par], W.park_cap), nra = min(cnt[C_PARKA0 + par], W.park_cap);
+    // exact roles: 64 walks per block to start with (16 per wave), at most half of the
+    // spill lanes and a quarter of the grid each
+    const int nrc = min(cnt[C_PARKC0 + (par ^ 1)], W.park_cap), nra = min(cnt[C_PARKA0 + (par ^ 1)], W.park_cap);
     const int ec = nrc + cnt[C_FBC0 + par], ea = nra + cnt[C_FBA0 + par];
-    const int half = W.spill_lanes / 512;
+    const int half = min(W.spill_lanes / 512, max(1, (int)gridDim.x / 4));
     const int nbe_c = min(half, (ec + 63) / 64), nbe_a = min(half, (ea + 63) / 64);
     const int b = (int)blockIdx.x;
     if (b < nbe_c) {
@@ -496,10 +484,59 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_OC
         return;
     }
     if (b < nbe_c + nbe_a) {
-        exact_any(W, par, s_lds, (half + b - nbe_c) * 256 + (int)threadIdx.x, nra, ea, ps);
+        exact_any(W, par, s_lds, (W.spill_lanes / 512 + b - nbe_c) * 256 + (int)threadIdx.x, nra, ea, ps);
         flush_stats<STATS>(st, stats);
         return;
     }
+    shard_prefix(cnt, RT_QSHARDS, [&](int j) { return ac_at(par, j); }, s_pre);
+    const int n = s_pre[RT_QSHARDS];
+    if (STATS && W.iterq && b == nbe_c + nbe_a && threadIdx.x == 0 && W.iter < RT_MAX_TIMED_ITERS)
+        W.iterq[2 * W.iter + 1] = n;
+    const int nbs = (int)gridDim.x - (nbe_c + nbe_a);
+    const int wg = (b - nbe_c - nbe_a) * (int)(blockDim.x >> 6) + (int)(threadIdx.x >> 6);
+    const int wn = nbs * (int)(blockDim.x >> 6);
+    for (int base = wg * 64; base < n; base += wn * 64) {
+        const int idx = base + lane_id();
+        rtk::Emit e;
+        e.mask = 0;
+        e.active = false;
+        int p = -1;
+        if (idx < n) {
+            const int sh = shard_find(s_pre, RT_QSHARDS, idx);
+            p = W.act_in[(size_t)sh * W.seg_cap + (idx - s_pre[sh])];
+            rtk::path_step(W, p, e, ps);
+        }
+        append_emit(W, par ^ 1, base, n, p, e);
+    }
+    flush_stats<STATS>(st, stats);
+}
+
+template <bool STATS>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_OCC, 8))) void k_trace(rtk::WaveView W, int par, unsigned long long* stats)
+{
+    __shared__ uint32_t s_lds[RT_LDS_WORDS * 256];
+    __shared__ int s_pre[rtk::RK_COUNT * RT_QSHARDS + 1];
+    int32_t* cnt = W.counters;
+    if (blockIdx.x == 0) {  // filled by k_step(i) next
+        for (int j = threadIdx.x; j < (rtk::RK_COUNT + 1) * RT_QSHARDS; j += blockDim.x)
+            cnt[j < rtk::RK_COUNT * RT_QSHARDS ? qc_at(par ^ 1, j / RT_QSHARDS, j % RT_QSHARDS)
+                                                : ac_at(par ^ 1, j - rtk::RK_COUNT * RT_QSHARDS)] = 0;
+        if (threadIdx.x == 0) {
+            cnt[C_PARKC0 + par] = cnt[C_PARKA0 + par] = 0;
+            cnt[C_TK_EXACT_C] = cnt[C_TK_EXACT_A] = 0;
+        }
+    }
+    // release the paths whose exact walks k_step(i - 1) finished
+    {
+        const int nd = cnt[C_DONE0 + (par ^ 1)];
+        for (int j = (int)(blockIdx.x * blockDim.x + threadIdx.x); j < nd; j += (int)(gridDim.x * blockDim.x))
+            atomicSub(&W.r_park[W.done[par ^ 1][j]], 1);
+    }
+    rtk::Stats st;
+    if (STATS)
+        for (int i = 0; i < RT_STAT_COUNT; i++) st.c[i] = 0;
+    rtk::Stats* ps = STATS ? &st : nullptr;
+    const int b = (int)blockIdx.x;
 
     // fast roles: a quad of lanes per query (rt_quad.h), 16 queries per wave
     const int sub = (int)(threadIdx.x & 3);
@@ -511,9 +548,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_OC
     const int c0 = s_pre[rtk::RK_CONT * RT_QSHARDS], a0 = s_pre[rtk::RK_ESH * RT_QSHARDS];
     const int nc = s_pre[(last_kind + 1) * RT_QSHARDS] - c0;
     const int na = W.any_rays ? s_pre[(rtk::RK_BENV + 1) * RT_QSHARDS] - a0 : 0;
-    if (STATS && W.iterq && b == nbe_c + nbe_a && threadIdx.x == 0 && W.iter < RT_MAX_TIMED_ITERS)
-        W.iterq[2 * W.iter] = nc + na + ec + ea;
-    const int fb0 = nbe_c + nbe_a, nbf = (int)gridDim.x - fb0;
+    if (STATS && W.iterq && b == 0 && threadIdx.x == 0 && W.iter < RT_MAX_TIMED_ITERS) W.iterq[2 * W.iter] = nc + na;
+    const int fb0 = 0, nbf = (int)gridDim.x;
     const int nbc = split_blocks(nbf, nc, na);
     const bool closest = b - fb0 < nbc;
     const int rb = closest ? b - fb0 : b - fb0 - nbc;                       // block index within the role
@@ -521,8 +557,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_OC
     const int wg = rb * (int)(blockDim.x >> 6) + (int)(threadIdx.x >> 6);  // wave index within the role
     const int wn = rnb * (int)(blockDim.x >> 6);
     const int total = closest ? nc : na;
-    int32_t* fbn = cnt + (closest ? C_FBC0 : C_FBA0) + (par ^ 1);
-    rtk::RayRec* fbl = closest ? W.fb_c[par ^ 1] : W.fb_a[par ^ 1];
+    int32_t* fbn = cnt + (closest ? C_FBC0 : C_FBA0) + par;  // walked exactly by k_step(i)
+    rtk::RayRec* fbl = closest ? W.fb_c[par] : W.fb_a[par];
     for (int base = wg * 16; base < total; base += wn * 16) {
         const int idx = base + (lane_id() >> 2);
         bool fail = false;
@@ -1125,8 +1161,8 @@ static int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounce
         if (kind == 2) {  // (a fallback pending: step, then the live count, checked again next iteration)
             const int par = La.it & 1;
             const int32_t* f = La.h + act_bytes / 4;
-            if (f[C_FBC0 + (par ^ 1)] == 0 && f[C_FBA0 + (par ^ 1)] == 0 && f[C_PARKC0 + (par ^ 1)] == 0 &&
-                f[C_PARKA0 + (par ^ 1)] == 0) {
+            if (f[C_FBC0 + par] == 0 && f[C_FBA0 + par] == 0 && f[C_PARKC0 + (par ^ 1)] == 0 &&
+                f[C_PARKA0 + (par ^ 1)] == 0) {  // (k_trace(i) released DONE[par ^ 1])
                 // few paths left and none waits: the tail kernel finishes them all
                 HIPCHK(c, hipMemsetAsync(La.cnt + C_TK_TAIL, 0, 4, La.s));
                 if (S)

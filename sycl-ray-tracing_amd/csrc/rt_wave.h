@@ -102,6 +102,7 @@ struct WaveView {
     RayRec* fb_c[2];        // [5 n_slots] closest-hit queries left to the exact walk (d.w = kind), by parity
     RayRec* fb_a[2];        // [2 n_slots] occlusion queries left to the exact walk, by parity
     ParkC* park_c[2];       // parked closest-hit queries, double-buffered by iteration parity
+    int32_t* done[2];       // slots whose exact walks finished, by parity (released by the next k_trace)
     ParkA* park_a[2];
     int park_cap;
     int budget;             // steps a query may take per launch before it parks
@@ -167,6 +168,7 @@ inline size_t wave_carve(char* base, size_t n, WaveView& W)  // uses W.park_cap,
         W.fb_a[k] = (RayRec*)take(2 * n * sizeof(RayRec));
         W.park_c[k] = (ParkC*)take((size_t)W.park_cap * sizeof(ParkC));
         W.park_a[k] = (ParkA*)take((size_t)W.park_cap * sizeof(ParkA));
+        W.done[k] = (int32_t*)take((7 * n + 2 * (size_t)W.park_cap) * 4);
     }
     W.spill_r = (uint32_t*)take((size_t)W.spill_lanes * RT_STACK_CAP * 4);
     W.spill_k = (float*)take((size_t)W.spill_lanes * RT_STACK_CAP * 4);
