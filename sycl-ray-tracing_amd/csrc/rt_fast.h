@@ -137,7 +137,9 @@ RT_HD void sort4(float* k, int* v)
 }
 
 // Relative width of the window past t* in which other hits are collected.
+#ifndef RT_T2_WINDOW
 #define RT_T2_WINDOW 1.0e-3f
+#endif
 
 // Search-BVH walk: 1 = one item (node or leaf) per trip (fast_closest_u /
 // fast_any_u), 0 = one node per trip with its leaf children inline.
