@@ -70,6 +70,7 @@ struct RtSceneView {
     const float4_* tri4;
     const int32_t* prim2k;
     const int32_t* mat_idx;
+    const int32_t* matk;  // leaf-order triangle k -> mat_idx[prim of k] (device: one load instead of two)
     const RtMat* mats;
     const int32_t* emissive;
     const float4_* spheres;  // 2 records each: {c.xyz, r}, {prim bits, 0, 0, 0}

@@ -95,7 +95,7 @@ __host__ __device__ __forceinline__ int ac_at(int par, int shard)
 
 struct Backend {
     DevBuf nodes, tri4, prim2k, mat_idx, mats, emissive, spheres, env, env_lum, cdf;
-    DevBuf bvh4, bvh_tri4, parent, leaf_of, cdf_row, cdf_coarse, cdf_fence;
+    DevBuf bvh4, bvh_tri4, parent, leaf_of, cdf_row, cdf_coarse, cdf_fence, matk;
     DevBuf stats;     // 2 x RT_STAT_COUNT u64: all kernels, then the tail kernel's share
     DevBuf iterq;     // stats renders: per-iteration {queries, live slots} (RT_ITER_LOG)
     DevBuf wave[RT_MAX_LANES];      // per lane: path state, pending records, results, queues, lists
@@ -902,7 +902,7 @@ void rt_backend_destroy(rt_context* c)
     (void)hipSetDevice(c->device);
     DevBuf* all[] = {&b->nodes, &b->tri4, &b->prim2k, &b->mat_idx, &b->mats, &b->emissive, &b->spheres, &b->env,
                      &b->env_lum, &b->cdf, &b->bvh4, &b->bvh_tri4, &b->parent, &b->leaf_of, &b->cdf_row, &b->cdf_coarse,
-                     &b->cdf_fence, &b->stats, &b->xy, &b->fb};
+                     &b->cdf_fence, &b->matk, &b->stats, &b->xy, &b->fb};
     for (DevBuf* d : all)
         if (d->p) (void)hipFree(d->p);
     for (int l = 0; l < RT_MAX_LANES; l++)
@@ -929,6 +929,13 @@ int rt_backend_upload(rt_context* c)
 {
     Backend* b = be(c);
     HIPCHK(c, hipSetDevice(c->device));
+    // material index of each leaf-order triangle k: mat_idx[prim(k)] (rt_trace.h load_mat_hit)
+    std::vector<int32_t> matk(c->flat.tri4.size() / 3);
+    for (size_t k = 0; k < matk.size(); k++) {
+        int32_t prim;
+        std::memcpy(&prim, &c->flat.tri4[3 * k].w, 4);
+        matk[k] = c->mat_idx[prim];
+    }
     int r = 0;
     if ((r = upload(c, b->nodes, c->flat.nodes)) || (r = upload(c, b->tri4, c->flat.tri4)) ||
         (r = upload(c, b->prim2k, c->flat.prim2k)) || (r = upload(c, b->mat_idx, c->mat_idx)) ||
@@ -938,7 +945,7 @@ int rt_backend_upload(rt_context* c)
         (r = upload(c, b->bvh4, c->flat.bvh4)) || (r = upload(c, b->bvh_tri4, c->flat.bvh_tri4)) ||
         (r = upload(c, b->parent, c->flat.parent)) || (r = upload(c, b->leaf_of, c->flat.leaf_of)) ||
         (r = upload(c, b->cdf_row, c->cdf_row)) || (r = upload(c, b->cdf_coarse, c->cdf_coarse)) ||
-        (r = upload(c, b->cdf_fence, c->cdf_fence)) ||
+        (r = upload(c, b->cdf_fence, c->cdf_fence)) || (r = upload(c, b->matk, matk)) ||
         (r = ensure(c, b->stats, 2 * RT_STAT_COUNT * sizeof(unsigned long long))))
         return r;
     for (int l = 0; l < RT_MAX_LANES; l++)
@@ -948,6 +955,7 @@ int rt_backend_upload(rt_context* c)
     v.tri4 = (const float4_*)b->tri4.p;
     v.prim2k = (const int32_t*)b->prim2k.p;
     v.mat_idx = (const int32_t*)b->mat_idx.p;
+    v.matk = (const int32_t*)b->matk.p;
     v.mats = (const RtMat*)b->mats.p;
     v.emissive = (const int32_t*)b->emissive.p;
     v.spheres = (const float4_*)b->spheres.p;

@@ -698,6 +698,13 @@ RT_HD Mat load_mat(const RtSceneView& S, int prim)
     const RtMat m = S.mats[S.mat_idx[prim]];
     return Mat{Col{m.er, m.eg, m.eb}, Col{m.dr, m.dg, m.db}, m.metalness, m.roughness};
 }
+// The material of a hit: for a triangle (leaf-order k >= 0) through matk[k],
+// the same entry as mat_idx[prim] (built at upload), without the dependent load.
+RT_HD Mat load_mat_hit(const RtSceneView& S, int k, int prim)
+{
+    const RtMat m = S.mats[(k >= 0 && S.matk) ? S.matk[k] : S.mat_idx[prim]];
+    return Mat{Col{m.er, m.eg, m.eb}, Col{m.dr, m.dg, m.db}, m.metalness, m.roughness};
+}
 
 RT_HD V3 rotate_around_normal(V3 n, V3 l)  // render_kernel.cpp:5-22
 {

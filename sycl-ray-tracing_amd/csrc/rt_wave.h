@@ -357,7 +357,7 @@ RT_HD void shade(const WaveView& W, int p, PathReg& P, const Hit& h, Emit& e, St
 {
     const RtSceneView& S = W.S;
     if (st) st->c[RT_STAT_MAT]++;
-    const Mat m = load_mat(S, h.prim);
+    const Mat m = load_mat_hit(S, h.k, h.prim);
     const V3 rd = P.rd;
     uint32_t fl = PF_AUX;
 
@@ -491,6 +491,9 @@ RT_HD void resolve(const WaveView& W, int p, PathReg& P, Stats* st)
 {
     const RtSceneView& S = W.S;
     const uint32_t fl = P.flags;
+    // the records every resolve reads, loaded together up front (one memory round trip)
+    const float4_ q_thr = W.q_thr[p], q_env = W.q_env[p], q_benv = W.q_benv[p];
+    const uint8_t r_esh = W.r_esh[p], r_benv = W.r_benv[p];
     Col light = col(0.0f);
     if (fl & PF_LSH) {
         const float4_ q = W.q_light[p];
@@ -511,7 +514,7 @@ RT_HD void resolve(const WaveView& W, int p, PathReg& P, Stats* st)
             float ca = rt_max(dot(nh.n, neg(sdir)), 0.0f);
             if (ca > 0.0f) {
                 if (st) st->c[RT_STAT_MAT]++;
-                const Mat mm = load_mat(S, nh.prim);
+                const Mat mm = load_mat_hit(S, nh.k, nh.prim);
                 const Col e = mm.emission;
                 if (e.r > 0 || e.g > 0 || e.b > 0) {
                     float d2 = t * t;
@@ -528,12 +531,12 @@ RT_HD void resolve(const WaveView& W, int p, PathReg& P, Stats* st)
         }
     }
     Col env_sample = col(0.0f), brdf_sample = col(0.0f);
-    if ((fl & PF_ESH) && !W.r_esh[p]) env_sample = colof(W.q_env[p]);
-    if ((fl & PF_BENV) && !W.r_benv[p]) brdf_sample = colof(W.q_benv[p]);
+    if ((fl & PF_ESH) && !r_esh) env_sample = colof(q_env);
+    if ((fl & PF_BENV) && !r_benv) brdf_sample = colof(q_benv);
     const Col lr = cadd(light, bmis);
     const Col er = cadd(brdf_sample, env_sample);
     if (fl & PF_EMIT0) P.sc = cadd(P.sc, colof(W.q_em[p]));
-    P.sc = cadd(P.sc, cmul(cadd(lr, er), colof(W.q_thr[p])));
+    P.sc = cadd(P.sc, cmul(cadd(lr, er), colof(q_thr)));
 }
 
 // One iteration of path slot p: resolve the bounce shaded last iteration,
@@ -543,17 +546,19 @@ RT_HD void path_step(const WaveView& W, int p, Emit& e, Stats* st)
 {
     e.mask = 0;
     e.active = true;
-    if (W.r_park[p] != 0) return;  // a query of this path is parked: wait
+    // the slot's state, wait count and continuation result in one round trip
+    const int park = W.r_park[p];
     PathReg P;
     load_path(W, p, P);
-    e.mask = 0;
-    e.active = true;
+    const float cont_t = W.r_cont_t[p];
+    const int cont_k = W.r_cont_k[p];
+    if (park != 0) return;  // a query of this path is parked: wait
     if (P.flags & PF_AUX) resolve(W, p, P, st);
     bool end = (P.flags & PF_END) != 0;
     if (P.flags & PF_CONT) {
-        const float t = W.r_cont_t[p];
+        const float t = cont_t;
         Hit h;
-        if (hit_from(W.S, P.ro, P.rd, t, W.r_cont_k[p], h)) {
+        if (hit_from(W.S, P.ro, P.rd, t, cont_k, h)) {
             shade(W, p, P, h, e, st);
             store_path(W, p, P);
             return;
