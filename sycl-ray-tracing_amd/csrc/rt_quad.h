@@ -345,4 +345,128 @@ __device__ int quad_query_any(const RtSceneView& S, V3 o, V3 d, QSTK& stk, int s
     }
 }
 
+// One walk loop for a wave whose quads carry both kinds of query (the tail
+// kernel's closest and occlusion lists in one pass): a quad with anyq false
+// answers as quad_query_closest (1 with t, k; -1: exact walk), one with anyq
+// true as quad_query_any (1 / 0; -1: exact walk). The occlusion answer does
+// not depend on the visit order (any hit whose octree chain holds), so both
+// kinds descend nearest-first; an occlusion quad keeps no window (tmax inf).
+template <class QSTK>
+__device__ int quad_query_mixed(const RtSceneView& S, V3 o, V3 d, QSTK& stk, int sub, bool anyq, float& t_out,
+                                int& k_out, Stats* st)
+{
+    if (st && sub == 0) st->c[anyq ? RT_STAT_ANY_RAYS : RT_STAT_RAYS]++;
+    t_out = -1.0f;
+    k_out = -1;
+    if (rt_isnan(d.x) || rt_isnan(d.y) || rt_isnan(d.z) || rt_isnan(o.x) || rt_isnan(o.y) || rt_isnan(o.z))
+        return anyq ? 0 : 1;
+    FastHit h;
+    h.t = __builtin_inff();
+    h.t2 = __builtin_inff();
+    h.k = -1;
+    h.leaf = -1;
+    h.prim = 0x7fffffff;
+    h.tie = false;
+    const RayB rb = rayb_setup(o, d);
+    int sp = 0;
+    int cur = 0;
+    for (;;) {
+        if (cur >= 0) {
+            if (st && sub == 0) st->c[anyq ? RT_STAT_ANY_VOL : RT_STAT_VOL] += 4;
+            const float tmax = anyq ? __builtin_inff() : h.t + h.t * RT_T2_WINDOW;
+            const QChild c = quad_child(S, cur, sub, rb, tmax);
+            const float key = c.ok ? c.tn : __builtin_inff();
+            const float k1 = qdppf<RT_QX1>(key), k2 = qdppf<RT_QX2>(key), k3 = qdppf<RT_QX3>(key);
+            const int s1 = sub ^ 1, s2 = sub ^ 2, s3 = sub ^ 3;
+            const int rank = (k1 < key || (k1 == key && s1 < sub) ? 1 : 0) + (k2 < key || (k2 == key && s2 < sub) ? 1 : 0) +
+                             (k3 < key || (k3 == key && s3 < sub) ? 1 : 0);
+            const int nv = qsum(c.ok ? 1 : 0);
+            if (sp + nv - 1 > QSTK::CAP) return -1;
+            if (c.ok && rank > 0) stk.set(sp + nv - 1 - rank, (uint32_t)c.item, key);
+            if (nv > 0) {
+                sp += nv - 1;
+                cur = qor(c.ok && rank == 0 ? c.item : 0);
+                continue;
+            }
+        } else {
+            if (st && sub == 0) st->c[anyq ? RT_STAT_ANY_TRI : RT_STAT_TRI] += ((~cur) & 3) + 1;
+            int k, leaf, prim;
+            const float tv = quad_tri(S, cur, sub, o, d, k, leaf, prim);
+            if (anyq) {
+                const int hitb = tv < __builtin_inff() ? 1 : 0;
+                if (S.brute) {
+                    if (qor(hitb)) return 1;
+                } else {
+                    const int h1 = qdpp<RT_QX1>(hitb), h2 = qdpp<RT_QX2>(hitb), h3 = qdpp<RT_QX3>(hitb);
+                    const int l1 = qdpp<RT_QX1>(leaf), l2 = qdpp<RT_QX2>(leaf), l3 = qdpp<RT_QX3>(leaf);
+#pragma unroll
+                    for (int j = 0; j < 4; j++) {
+                        const int x = j ^ sub;
+                        const int hj = x == 0 ? hitb : x == 1 ? h1 : x == 2 ? h2 : h3;
+                        if (!hj) continue;
+                        const int lj = x == 0 ? leaf : x == 1 ? l1 : x == 2 ? l2 : l3;
+                        if (quad_chain_ok(S, o, d, lj, false, 0.0f, sub, st)) return 1;
+                    }
+                }
+            } else {
+                float m1 = tv, m2 = __builtin_inff();
+                {
+                    const float o1 = qdppf<RT_QX1>(m1), o2 = qdppf<RT_QX1>(m2);
+                    const float n1 = __builtin_fminf(m1, o1), n2 = __builtin_fminf(__builtin_fmaxf(m1, o1), __builtin_fminf(m2, o2));
+                    m1 = n1, m2 = n2;
+                }
+                {
+                    const float o1 = qdppf<RT_QX2>(m1), o2 = qdppf<RT_QX2>(m2);
+                    const float n1 = __builtin_fminf(m1, o1), n2 = __builtin_fminf(__builtin_fmaxf(m1, o1), __builtin_fminf(m2, o2));
+                    m1 = n1, m2 = n2;
+                }
+                int pm = tv == m1 ? prim : 0x7fffffff;
+                pm = min(pm, qdpp<RT_QX1>(pm));
+                pm = min(pm, qdpp<RT_QX2>(pm));
+                const bool mine = tv == m1 && prim == pm;
+                if (m1 < h.t) {
+                    h.t2 = __builtin_fminf(h.t, m2);
+                    h.t = m1;
+                    h.k = qor(mine ? k : 0);
+                    h.leaf = qor(mine ? leaf : 0);
+                    h.prim = pm;
+                    h.tie = m2 == m1;
+                } else if (m1 == h.t && m1 < __builtin_inff()) {
+                    h.tie = true;
+                    h.t2 = m1;
+                    if (pm < h.prim) {
+                        h.k = qor(mine ? k : 0);
+                        h.leaf = qor(mine ? leaf : 0);
+                        h.prim = pm;
+                    }
+                } else {
+                    h.t2 = __builtin_fminf(h.t2, m1);
+                }
+            }
+        }
+        const float tmax = anyq ? __builtin_inff() : h.t + h.t * RT_T2_WINDOW;
+        cur = 0x7fffffff;
+        while (sp > 0) {
+            --sp;
+            if (stk.key(sp) <= tmax) {
+                cur = (int)stk.rec(sp);
+                break;
+            }
+        }
+        if (cur == 0x7fffffff) break;
+    }
+    if (anyq || h.k < 0) return anyq ? 0 : 1;
+    if (S.brute) {
+        t_out = h.t;
+        k_out = h.k;
+        return 1;
+    }
+    if (h.tie) return -1;
+    const float t2 = __builtin_fminf(h.t2, h.t + h.t * RT_T2_WINDOW);
+    if (!quad_chain_ok(S, o, d, h.leaf, true, t2, sub, st)) return -1;
+    t_out = h.t;
+    k_out = h.k;
+    return 1;
+}
+
 }  // namespace rtk

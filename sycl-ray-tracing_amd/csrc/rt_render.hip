@@ -648,6 +648,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_OC
 // walk, so every path is ready to step; a query the quad walk cannot answer
 // is answered here by the exact walk, inline, by lane 0 of its quad.
 #define RT_TAIL_MAXP 16  // paths per wave at most (5 rays each: 80 per list)
+#ifndef RT_TAIL_MIXED
+#define RT_TAIL_MIXED 1  // closest and occlusion queries of a step in one pass (quad_query_mixed)
+#endif
 #ifndef RT_TAIL_OCC
 #define RT_TAIL_OCC 3    // k_tail waves per SIMD (2: no spills but half the paths per launch; 3 measured faster)
 #endif
@@ -714,6 +717,47 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TAIL_OCC
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the lists are read by other lanes
         __builtin_amdgcn_wave_barrier();
+#if RT_TAIL_MIXED
+        // trace: both lists in one index space, 16 queries (quads) per pass, each quad
+        // walking its own kind (quad_query_mixed): a step waits for its slowest query,
+        // not for the closest walk plus the occlusion walks after it
+        const int nq = nl[0] + nl[1];
+        for (int base = 0; base < nq; base += 16) {
+            const int qi = base + (lane >> 2);
+            if (qi < nq) {
+                const int l = qi < nl[0] ? 0 : 1;
+                const rtk::RayRec r = s_q[wv][l][l ? qi - nl[0] : qi];
+                const uint32_t target = rt_asuint(r.d.w);
+                const rtk::V3 o = rtk::v3of(r.o), d = rtk::v3of(r.d);
+                float t;
+                int k;
+                const int a = rtk::quad_query_mixed(W.S, o, d, stk, sub, l == 1, t, k, ps);
+                if (a >= 0 && sub == 0) {
+                    if (l == 0)
+                        rtk::finish_closest(W, target, o, d, t, k);
+                    else
+                        rtk::finish_any(W, target, a == 1);
+                }
+                if (a < 0 && sub == 0) {  // the exact octree walk, to completion
+                    if (STATS) st.c[RT_STAT_FALLBACK]++;
+                    xs.f = stk;
+                    if (l == 0) {
+                        rtk::TravC T;
+                        if (rtk::travc_begin(W.S, T, o, d, ps))
+                            while (rtk::travc_step(W.S, T, xs, ps)) {
+                            }
+                        rtk::finish_closest(W, target, T.o, T.d, T.best_t, T.best_k);
+                    } else {
+                        rtk::TravA T;
+                        if (rtk::trava_begin(W.S, T, o, d, ps))
+                            while (rtk::trava_step(W.S, T, xs, ps)) {
+                            }
+                        rtk::finish_any(W, target, T.hit);
+                    }
+                }
+            }
+        }
+#else
         // trace: closest list, then occlusion list, 16 queries (quads) per pass
         for (int l = 0; l < 2; l++) {
             for (int base = 0; base < nl[l]; base += 16) {
@@ -753,6 +797,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TAIL_OCC
                 }
             }
         }
+#endif
     }
     flush_stats<STATS>(st, stats);
     flush_stats<STATS>(st, stats + RT_STAT_COUNT);  // (the tail kernel's share, for per-kernel byte counts)
