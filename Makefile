@@ -71,3 +71,9 @@ clean:
 	rm -rf $(OBJ) $(LIB) build/libm_check oracle/liboracle.so
 
 .PHONY: all ref clean
+
+# experiment builds: make variant V=name DEFS="-DRT_TAIL_OCC=2" -> lib/librt_hip_name.so (RT_HIP_LIB=...)
+variant: $(OBJ)/rt_scene.host.o $(OBJ)/rt_imageio.host.o $(OBJ)/rt_capi_host.host.o
+	@mkdir -p $(LIB)
+	$(HIPCC) $(HIPFLAGS) $(DEFS) -c $(SRC)/rt_render.hip -o $(OBJ)/rt_render_$(V).o
+	$(HIPCC) -shared --offload-arch=$(ARCH) -fPIC $(OBJ)/rt_render_$(V).o $^ -o $(LIB)/librt_hip_$(V).so

@@ -345,128 +345,217 @@ __device__ int quad_query_any(const RtSceneView& S, V3 o, V3 d, QSTK& stk, int s
     }
 }
 
-// One walk loop for a wave whose quads carry both kinds of query (the tail
-// kernel's closest and occlusion lists in one pass): a quad with anyq false
-// answers as quad_query_closest (1 with t, k; -1: exact walk), one with anyq
-// true as quad_query_any (1 / 0; -1: exact walk). The occlusion answer does
-// not depend on the visit order (any hit whose octree chain holds), so both
-// kinds descend nearest-first; an occlusion quad keeps no window (tmax inf).
-template <class QSTK>
-__device__ int quad_query_mixed(const RtSceneView& S, V3 o, V3 d, QSTK& stk, int sub, bool anyq, float& t_out,
-                                int& k_out, Stats* st)
+// A quad walk as a state machine, one node or leaf visit per qwalk_step, so
+// that a wave can refill a quad with its next query the moment the quad's
+// walk ends instead of waiting for the wave's slowest walk (k_trace), and so
+// that closest and occlusion walks share one loop (k_tail). anyq false:
+// quad_query_closest's answer; anyq true: quad_query_any's. The occlusion
+// answer does not depend on the visit order (any hit whose octree chain
+// holds), so both kinds descend nearest-first; an occlusion walk keeps no
+// window (tmax inf). Every field is quad-uniform.
+struct QWalk {
+    V3 o, d;
+    RayB rb;
+    FastHit h;
+    int sp, cur;
+    bool anyq;
+    float t;  // answer: closest t (-1: no hit) ...
+    int k;    // ... and leaf-order triangle (-1: none); occlusion: 1 / 0
+};
+
+// Starts a walk. Returns 0 (walk with qwalk_step) or 1 when the answer is
+// already known (a NaN ray: no hit).
+__device__ __forceinline__ int qwalk_begin(QWalk& w, V3 o, V3 d, bool anyq, int sub, Stats* st)
 {
     if (st && sub == 0) st->c[anyq ? RT_STAT_ANY_RAYS : RT_STAT_RAYS]++;
-    t_out = -1.0f;
-    k_out = -1;
-    if (rt_isnan(d.x) || rt_isnan(d.y) || rt_isnan(d.z) || rt_isnan(o.x) || rt_isnan(o.y) || rt_isnan(o.z))
-        return anyq ? 0 : 1;
-    FastHit h;
-    h.t = __builtin_inff();
-    h.t2 = __builtin_inff();
-    h.k = -1;
-    h.leaf = -1;
-    h.prim = 0x7fffffff;
-    h.tie = false;
-    const RayB rb = rayb_setup(o, d);
-    int sp = 0;
-    int cur = 0;
-    for (;;) {
-        if (cur >= 0) {
-            if (st && sub == 0) st->c[anyq ? RT_STAT_ANY_VOL : RT_STAT_VOL] += 4;
-            const float tmax = anyq ? __builtin_inff() : h.t + h.t * RT_T2_WINDOW;
-            const QChild c = quad_child(S, cur, sub, rb, tmax);
-            const float key = c.ok ? c.tn : __builtin_inff();
-            const float k1 = qdppf<RT_QX1>(key), k2 = qdppf<RT_QX2>(key), k3 = qdppf<RT_QX3>(key);
-            const int s1 = sub ^ 1, s2 = sub ^ 2, s3 = sub ^ 3;
-            const int rank = (k1 < key || (k1 == key && s1 < sub) ? 1 : 0) + (k2 < key || (k2 == key && s2 < sub) ? 1 : 0) +
-                             (k3 < key || (k3 == key && s3 < sub) ? 1 : 0);
-            const int nv = qsum(c.ok ? 1 : 0);
-            if (sp + nv - 1 > QSTK::CAP) return -1;
-            if (c.ok && rank > 0) stk.set(sp + nv - 1 - rank, (uint32_t)c.item, key);
-            if (nv > 0) {
-                sp += nv - 1;
-                cur = qor(c.ok && rank == 0 ? c.item : 0);
-                continue;
+    w.o = o;
+    w.d = d;
+    w.anyq = anyq;
+    w.t = -1.0f;
+    w.k = anyq ? 0 : -1;
+    if (rt_isnan(d.x) || rt_isnan(d.y) || rt_isnan(d.z) || rt_isnan(o.x) || rt_isnan(o.y) || rt_isnan(o.z)) return 1;
+    w.h.t = __builtin_inff();
+    w.h.t2 = __builtin_inff();
+    w.h.k = -1;
+    w.h.leaf = -1;
+    w.h.prim = 0x7fffffff;
+    w.h.tie = false;
+    w.rb = rayb_setup(o, d);
+    w.sp = 0;
+    w.cur = 0;
+    return 0;
+}
+
+// The memory of one visit, loaded before it is used (qwalk_issue), so that a
+// caller can put other loads in flight beside it: inner node, lane sub's 32-B
+// child record (x0, x1); leaf, lane sub's 48-B triangle (x0, x1, x2).
+struct QVisit {
+    float4_ x0, x1, x2;
+};
+__device__ __forceinline__ void qwalk_issue(const QWalk& w, const RtSceneView& S, int sub, QVisit& v)
+{
+    if (w.cur >= 0) {
+        const float4_* p = (const float4_*)(S.bvh4 + w.cur) + 2 * sub;
+        v.x0 = p[0];
+        v.x1 = p[1];
+    } else {
+        const int it = ~w.cur;
+        if (sub <= (it & 3)) {
+            const float4_* p = S.bvh_tri4 + 3 * ((it >> 2) + sub);
+            v.x0 = p[0];
+            v.x1 = p[1];
+            v.x2 = p[2];
+        }
+    }
+}
+
+// One visit on the loaded records. Returns 0 while the walk goes on, 1 with
+// the answer in (t, k), -1 when the exact walk must answer (stack overflow, a
+// tie, a failed chain).
+template <class QSTK>
+__device__ int qwalk_consume(QWalk& w, const RtSceneView& S, QSTK& stk, int sub, const QVisit& v, Stats* st)
+{
+    const bool anyq = w.anyq;
+    FastHit& h = w.h;
+    if (w.cur >= 0) {
+        if (st && sub == 0) st->c[anyq ? RT_STAT_ANY_VOL : RT_STAT_VOL] += 4;
+        const float tmax = anyq ? __builtin_inff() : h.t + h.t * RT_T2_WINDOW;
+        QChild c;
+        {  // (quad_child on the loaded record)
+            const int ref = (int)rt_asuint(v.x1.z), cnt = (int)rt_asuint(v.x1.w);
+            const float mn[3] = {v.x0.x, v.x0.y, v.x0.z}, mx[3] = {v.x0.w, v.x1.x, v.x1.y};
+            c.ok = cnt >= 0 && box_hit(mn, mx, w.rb, tmax, c.tn) && c.tn <= tmax;
+            c.item = cnt > 0 ? leaf_item(ref, cnt) : ref;
+        }
+        const float key = c.ok ? c.tn : __builtin_inff();
+        // rank by (key, lane): the nearest hit child has rank 0
+        const float k1 = qdppf<RT_QX1>(key), k2 = qdppf<RT_QX2>(key), k3 = qdppf<RT_QX3>(key);
+        const int s1 = sub ^ 1, s2 = sub ^ 2, s3 = sub ^ 3;
+        const int rank = (k1 < key || (k1 == key && s1 < sub) ? 1 : 0) + (k2 < key || (k2 == key && s2 < sub) ? 1 : 0) +
+                         (k3 < key || (k3 == key && s3 < sub) ? 1 : 0);
+        const int nv = qsum(c.ok ? 1 : 0);
+        if (w.sp + nv - 1 > QSTK::CAP) return -1;
+        // far children on the stack, nearest of them on top
+        if (c.ok && rank > 0) stk.set(w.sp + nv - 1 - rank, (uint32_t)c.item, key);
+        if (nv > 0) {
+            w.sp += nv - 1;
+            w.cur = qor(c.ok && rank == 0 ? c.item : 0);
+            return 0;
+        }
+    } else {
+        if (st && sub == 0) st->c[anyq ? RT_STAT_ANY_TRI : RT_STAT_TRI] += ((~w.cur) & 3) + 1;
+        int k = -1, leaf = -1, prim = 0x7fffffff;
+        float tv = __builtin_inff();
+        {  // (quad_tri on the loaded record)
+            float t;
+            if (sub <= ((~w.cur) & 3) && tri_test_v(ld3(v.x0), ld3(v.x1), ld3(v.x2), w.o, w.d, t)) {
+                tv = t;
+                k = (int)rt_asuint(v.x0.w);
+                leaf = (int)rt_asuint(v.x1.w);
+                prim = (int)rt_asuint(v.x2.w);
             }
-        } else {
-            if (st && sub == 0) st->c[anyq ? RT_STAT_ANY_TRI : RT_STAT_TRI] += ((~cur) & 3) + 1;
-            int k, leaf, prim;
-            const float tv = quad_tri(S, cur, sub, o, d, k, leaf, prim);
-            if (anyq) {
-                const int hitb = tv < __builtin_inff() ? 1 : 0;
-                if (S.brute) {
-                    if (qor(hitb)) return 1;
-                } else {
-                    const int h1 = qdpp<RT_QX1>(hitb), h2 = qdpp<RT_QX2>(hitb), h3 = qdpp<RT_QX3>(hitb);
-                    const int l1 = qdpp<RT_QX1>(leaf), l2 = qdpp<RT_QX2>(leaf), l3 = qdpp<RT_QX3>(leaf);
-#pragma unroll
-                    for (int j = 0; j < 4; j++) {
-                        const int x = j ^ sub;
-                        const int hj = x == 0 ? hitb : x == 1 ? h1 : x == 2 ? h2 : h3;
-                        if (!hj) continue;
-                        const int lj = x == 0 ? leaf : x == 1 ? l1 : x == 2 ? l2 : l3;
-                        if (quad_chain_ok(S, o, d, lj, false, 0.0f, sub, st)) return 1;
-                    }
+        }
+        if (anyq) {
+            const int hitb = tv < __builtin_inff() ? 1 : 0;
+            if (S.brute) {
+                if (qor(hitb)) {  // USE_BVH 0: any triangle hit occludes
+                    w.k = 1;
+                    return 1;
                 }
             } else {
-                float m1 = tv, m2 = __builtin_inff();
-                {
-                    const float o1 = qdppf<RT_QX1>(m1), o2 = qdppf<RT_QX1>(m2);
-                    const float n1 = __builtin_fminf(m1, o1), n2 = __builtin_fminf(__builtin_fmaxf(m1, o1), __builtin_fminf(m2, o2));
-                    m1 = n1, m2 = n2;
+                // each hit lane's octree leaf in turn, checked by the whole quad
+                const int h1 = qdpp<RT_QX1>(hitb), h2 = qdpp<RT_QX2>(hitb), h3 = qdpp<RT_QX3>(hitb);
+                const int l1 = qdpp<RT_QX1>(leaf), l2 = qdpp<RT_QX2>(leaf), l3 = qdpp<RT_QX3>(leaf);
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    const int x = j ^ sub;
+                    const int hj = x == 0 ? hitb : x == 1 ? h1 : x == 2 ? h2 : h3;
+                    if (!hj) continue;
+                    const int lj = x == 0 ? leaf : x == 1 ? l1 : x == 2 ? l2 : l3;
+                    if (quad_chain_ok(S, w.o, w.d, lj, false, 0.0f, sub, st)) {
+                        w.k = 1;
+                        return 1;
+                    }
                 }
-                {
-                    const float o1 = qdppf<RT_QX2>(m1), o2 = qdppf<RT_QX2>(m2);
-                    const float n1 = __builtin_fminf(m1, o1), n2 = __builtin_fminf(__builtin_fmaxf(m1, o1), __builtin_fminf(m2, o2));
-                    m1 = n1, m2 = n2;
-                }
-                int pm = tv == m1 ? prim : 0x7fffffff;
-                pm = min(pm, qdpp<RT_QX1>(pm));
-                pm = min(pm, qdpp<RT_QX2>(pm));
-                const bool mine = tv == m1 && prim == pm;
-                if (m1 < h.t) {
-                    h.t2 = __builtin_fminf(h.t, m2);
-                    h.t = m1;
+            }
+        } else {
+            // quad (smallest, second smallest) of the lanes' hit distances
+            float m1 = tv, m2 = __builtin_inff();
+            {
+                const float o1 = qdppf<RT_QX1>(m1), o2 = qdppf<RT_QX1>(m2);
+                const float n1 = __builtin_fminf(m1, o1), n2 = __builtin_fminf(__builtin_fmaxf(m1, o1), __builtin_fminf(m2, o2));
+                m1 = n1, m2 = n2;
+            }
+            {
+                const float o1 = qdppf<RT_QX2>(m1), o2 = qdppf<RT_QX2>(m2);
+                const float n1 = __builtin_fminf(m1, o1), n2 = __builtin_fminf(__builtin_fmaxf(m1, o1), __builtin_fminf(m2, o2));
+                m1 = n1, m2 = n2;
+            }
+            // the lane holding m1 with the lowest original index
+            int pm = tv == m1 ? prim : 0x7fffffff;
+            pm = min(pm, qdpp<RT_QX1>(pm));
+            pm = min(pm, qdpp<RT_QX2>(pm));
+            const bool mine = tv == m1 && prim == pm;
+            if (m1 < h.t) {
+                h.t2 = __builtin_fminf(h.t, m2);
+                h.t = m1;
+                h.k = qor(mine ? k : 0);
+                h.leaf = qor(mine ? leaf : 0);
+                h.prim = pm;
+                h.tie = m2 == m1;
+            } else if (m1 == h.t && m1 < __builtin_inff()) {
+                h.tie = true;
+                h.t2 = m1;
+                if (pm < h.prim) {
                     h.k = qor(mine ? k : 0);
                     h.leaf = qor(mine ? leaf : 0);
                     h.prim = pm;
-                    h.tie = m2 == m1;
-                } else if (m1 == h.t && m1 < __builtin_inff()) {
-                    h.tie = true;
-                    h.t2 = m1;
-                    if (pm < h.prim) {
-                        h.k = qor(mine ? k : 0);
-                        h.leaf = qor(mine ? leaf : 0);
-                        h.prim = pm;
-                    }
-                } else {
-                    h.t2 = __builtin_fminf(h.t2, m1);
                 }
+            } else {
+                h.t2 = __builtin_fminf(h.t2, m1);
             }
         }
-        const float tmax = anyq ? __builtin_inff() : h.t + h.t * RT_T2_WINDOW;
-        cur = 0x7fffffff;
-        while (sp > 0) {
-            --sp;
-            if (stk.key(sp) <= tmax) {
-                cur = (int)stk.rec(sp);
-                break;
-            }
+    }
+    // pop, dropping entries the window has closed behind
+    const float tmax = anyq ? __builtin_inff() : h.t + h.t * RT_T2_WINDOW;
+    int nxt = 0x7fffffff;
+    while (w.sp > 0) {
+        --w.sp;
+        if (stk.key(w.sp) <= tmax) {
+            nxt = (int)stk.rec(w.sp);
+            break;
         }
-        if (cur == 0x7fffffff) break;
     }
-    if (anyq || h.k < 0) return anyq ? 0 : 1;
-    if (S.brute) {
-        t_out = h.t;
-        k_out = h.k;
-        return 1;
+    w.cur = nxt;
+    if (nxt != 0x7fffffff) return 0;
+    // the walk is over
+    if (anyq || h.k < 0) return 1;  // (t, k) = (-1, -1) / occlusion 0
+    if (!S.brute) {                  // USE_BVH 0: the closest M-T hit, lowest index on ties; no octree
+        if (h.tie) return -1;
+        const float t2 = __builtin_fminf(h.t2, h.t + h.t * RT_T2_WINDOW);
+        if (!quad_chain_ok(S, w.o, w.d, h.leaf, true, t2, sub, st)) return -1;
     }
-    if (h.tie) return -1;
-    const float t2 = __builtin_fminf(h.t2, h.t + h.t * RT_T2_WINDOW);
-    if (!quad_chain_ok(S, o, d, h.leaf, true, t2, sub, st)) return -1;
-    t_out = h.t;
-    k_out = h.k;
+    w.t = h.t;
+    w.k = h.k;
     return 1;
+}
+
+template <class QSTK>
+__device__ __forceinline__ int qwalk_step(QWalk& w, const RtSceneView& S, QSTK& stk, int sub, Stats* st)
+{
+    QVisit v;
+    qwalk_issue(w, S, sub, v);
+    return qwalk_consume(w, S, stk, sub, v, st);
+}
+
+// A whole walk (k_tail: a wave's closest and occlusion queries in one loop).
+// Returns 1 with (t, k) or the occlusion answer in k, -1: exact walk.
+template <class QSTK>
+__device__ int quad_query_mixed(const RtSceneView& S, V3 o, V3 d, QSTK& stk, int sub, bool anyq, QWalk& w, Stats* st)
+{
+    int r = qwalk_begin(w, o, d, anyq, sub, st);
+    while (r == 0) r = qwalk_step(w, S, stk, sub, st);
+    return r;
 }
 
 }  // namespace rtk

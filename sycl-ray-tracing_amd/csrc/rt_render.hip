@@ -675,6 +675,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TAIL_OCC
     const int last_kind = W.any_rays ? rtk::RK_BL : rtk::RK_BENV;
     int my = -1;
     bool drained = false;
+    int rounds = 0;  // (RT_ITER_LOG: the longest pool loop of the launch)
+    long long tk_step = 0, tk_walk = 0;  // (RT_ITER_LOG: 100 MHz ticks in path_step / in the walks)
+    const bool probe = STATS && W.iterq && W.iter + 1 < RT_MAX_TIMED_ITERS;
     for (;;) {
         // refill the wave's pool from the live list
         const bool need = lane < P && my < 0;
@@ -692,13 +695,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TAIL_OCC
             }
         }
         if (!__any(my >= 0)) break;
+        rounds++;
         // step
         rtk::Emit e;
         e.mask = 0;
         e.active = false;
+        const long long t0 = probe ? wall_clock64() : 0;
         if (my >= 0) {
             rtk::path_step(W, my, e, ps);
             if (!e.active) my = -1;
+        }
+        long long t1 = 0;
+        if (probe) {
+            t1 = wall_clock64();
+            tk_step += __shfl(t1, 0) - __shfl(t0, 0);
         }
         // emitted rays -> the wave's LDS lists
         int nl[2] = {0, 0};
@@ -729,14 +739,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TAIL_OCC
                 const rtk::RayRec r = s_q[wv][l][l ? qi - nl[0] : qi];
                 const uint32_t target = rt_asuint(r.d.w);
                 const rtk::V3 o = rtk::v3of(r.o), d = rtk::v3of(r.d);
-                float t;
-                int k;
-                const int a = rtk::quad_query_mixed(W.S, o, d, stk, sub, l == 1, t, k, ps);
+                rtk::QWalk qw;
+                const int a = rtk::quad_query_mixed(W.S, o, d, stk, sub, l == 1, qw, ps);
                 if (a >= 0 && sub == 0) {
                     if (l == 0)
-                        rtk::finish_closest(W, target, o, d, t, k);
+                        rtk::finish_closest(W, target, o, d, qw.t, qw.k);
                     else
-                        rtk::finish_any(W, target, a == 1);
+                        rtk::finish_any(W, target, qw.k == 1);
                 }
                 if (a < 0 && sub == 0) {  // the exact octree walk, to completion
                     if (STATS) st.c[RT_STAT_FALLBACK]++;
@@ -756,6 +765,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TAIL_OCC
                     }
                 }
             }
+        }
+        if (probe) {
+            const long long t2 = wall_clock64();
+            tk_walk += __shfl(t2, 0) - __shfl(t1, 0);
         }
 #else
         // trace: closest list, then occlusion list, 16 queries (quads) per pass
@@ -798,6 +811,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TAIL_OCC
             }
         }
 #endif
+    }
+    if (STATS && W.iterq && lane == 0 && W.iter < RT_MAX_TIMED_ITERS) atomicMax(W.iterq + 2 * W.iter + 1, rounds);
+    if (probe && lane == 0) {
+        atomicAdd(W.iterq + 2 * W.iter + 2, (int)(tk_step >> 4));
+        atomicAdd(W.iterq + 2 * W.iter + 3, (int)(tk_walk >> 4));
     }
     flush_stats<STATS>(st, stats);
     flush_stats<STATS>(st, stats + RT_STAT_COUNT);  // (the tail kernel's share, for per-kernel byte counts)
@@ -1070,7 +1088,7 @@ static int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounce
     const int rows = src.xy ? 0 : n / src.W;
     while (nl > 1 && (n < nl * 65536 || (!src.xy && rows < nl))) nl--;
     WaveLane L[RT_MAX_LANES];
-    int tail_p = 4;
+    int tail_p = 5;  // (5 paths: 15 queries, one pass of the wave's 16 quads; sweep 2-6 within 1 %)
     if (const char* e = getenv("RT_TAIL_PATHS")) tail_p = std::min(RT_TAIL_MAXP, std::max(0, atoi(e)));
     const int tail_blocks = dev_cus * RT_TAIL_OCC;  // one grid-fill of k_tail
     const long tail_max = (long)tail_blocks * 4 * tail_p / nl;
@@ -1272,7 +1290,7 @@ static int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounce
         HIPCHK(c, hipMemcpyAsync(hq.data(), b->iterq.p, hq.size() * 4, hipMemcpyDeviceToHost, s));
         HIPCHK(c, hipStreamSynchronize(s));
         if (FILE* f = fopen((std::string(iter_log) + ".counts").c_str(), "w")) {
-            for (int i = 0; i < L[0].it && i < RT_MAX_TIMED_ITERS; i++) fprintf(f, "%d %d %d\n", i, hq[2 * i], hq[2 * i + 1]);
+            for (int i = 0; i <= L[0].it && i < RT_MAX_TIMED_ITERS; i++) fprintf(f, "%d %d %d\n", i, hq[2 * i], hq[2 * i + 1]);
             fclose(f);
         }
     }
