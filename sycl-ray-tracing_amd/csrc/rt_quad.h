@@ -56,6 +56,15 @@ __device__ __forceinline__ int qsum(int v)
     return v + qdpp<RT_QX2>(v);
 }
 
+// Marks loaded values as needed here: the compiler issues a record's loads together
+// and waits once, instead of sinking part of them behind the first branch that reads
+// the rest (a second, serial memory round trip per visit).
+__device__ __forceinline__ void rt_pin(float4_ v) { asm volatile("" ::"v"(v.x), "v"(v.y), "v"(v.z), "v"(v.w)); }
+__device__ __forceinline__ void rt_pin(float a, float b, float c, float d, int e)
+{
+    asm volatile("" ::"v"(a), "v"(b), "v"(c), "v"(d), "v"(e));
+}
+
 // Per-quad stack in LDS: entry i of quad q at [i * QPB + q].
 template <int N, int QPB>
 struct QuadStack {
@@ -82,6 +91,8 @@ __device__ __forceinline__ QChild quad_child(const RtSceneView& S, int node, int
 {
     const float4_* p = (const float4_*)(S.bvh4 + node) + 2 * sub;
     const float4_ a = p[0], b = p[1];
+    rt_pin(a);
+    rt_pin(b);
     const int ref = (int)rt_asuint(b.z), cnt = (int)rt_asuint(b.w);
     const float mn[3] = {a.x, a.y, a.z}, mx[3] = {a.w, b.x, b.y};
     QChild c;
@@ -104,6 +115,9 @@ __device__ __forceinline__ float quad_tri(const RtSceneView& S, int item, int su
     if (sub < cnt) {
         const float4_* p = S.bvh_tri4 + 3 * (first + sub);
         const float4_ a = p[0], e1 = p[1], e2 = p[2];
+        rt_pin(a);
+        rt_pin(e1);
+        rt_pin(e2);
         float t;
         if (tri_test_v(ld3(a), ld3(e1), ld3(e2), o, d, t)) {
             tv = t;
@@ -237,6 +251,8 @@ __device__ __forceinline__ bool quad_chain_ok(const RtSceneView& S, V3 o, V3 d, 
         if (st && sub == 0) st->c[RT_STAT_VERIFY]++;
         const float* nd = (const float*)(S.nodes + rec);  // RtNode: dn[7], df[7], ref, cnt
         const float dn0 = nd[p0], df0 = nd[7 + p0], dn1 = nd[p1 < 7 ? p1 : 0], df1 = nd[7 + (p1 < 7 ? p1 : 0)];
+        const int par = S.parent[rec];
+        rt_pin(dn0, df0, dn1, df1, par);
         float tn = -__builtin_inff(), tf = __builtin_inff();
         {
             const bool neg = r0 < 0.0;
@@ -257,7 +273,6 @@ __device__ __forceinline__ bool quad_chain_ok(const RtSceneView& S, V3 o, V3 d, 
         tf = rt_min(tf, qdppf<RT_QX1>(tf));
         tf = rt_min(tf, qdppf<RT_QX2>(tf));
         if (tf < tn) return false;
-        const int par = S.parent[rec];
         if (par < 0) return true;
         if (need_t2 && !(t2 >= tn)) return false;
         if (S.chain_monotone) return true;
@@ -398,6 +413,8 @@ __device__ __forceinline__ void qwalk_issue(const QWalk& w, const RtSceneView& S
         const float4_* p = (const float4_*)(S.bvh4 + w.cur) + 2 * sub;
         v.x0 = p[0];
         v.x1 = p[1];
+        rt_pin(v.x0);
+        rt_pin(v.x1);
     } else {
         const int it = ~w.cur;
         if (sub <= (it & 3)) {
@@ -405,6 +422,9 @@ __device__ __forceinline__ void qwalk_issue(const QWalk& w, const RtSceneView& S
             v.x0 = p[0];
             v.x1 = p[1];
             v.x2 = p[2];
+            rt_pin(v.x0);
+            rt_pin(v.x1);
+            rt_pin(v.x2);
         }
     }
 }

@@ -576,7 +576,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_OC
             const int g = (closest ? c0 : a0) + idx;
             const int seg = shard_find(s_pre, rtk::RK_COUNT * RT_QSHARDS, g);
             const int kind = seg / RT_QSHARDS;
-            r = W.q[kind][(size_t)(seg % RT_QSHARDS) * W.seg_cap + (g - s_pre[seg])];
+            // (the queue base by selects: W.q[kind] with a lane-varying kind would be a load)
+            rtk::RayRec* qk = W.q[0];
+#pragma unroll
+            for (int k2 = 1; k2 < rtk::RK_COUNT; k2++) qk = kind == k2 ? W.q[k2] : qk;
+            r = qk[(size_t)(seg % RT_QSHARDS) * W.seg_cap + (g - s_pre[seg])];
             target = (rt_asuint(r.o.w) << 3) | (uint32_t)kind;
             if (closest) {
                 float t;
