@@ -17,9 +17,18 @@
 
 #include <stdint.h>
 
+#include "rt_fp.h"
+
 struct alignas(16) float4_ {
     float x, y, z, w;
 };
+RT_HD void rt_pin(float4_ v)  // (rt_fp.h rt_pin, per component)
+{
+    rt_pin(v.x);
+    rt_pin(v.y);
+    rt_pin(v.z);
+    rt_pin(v.w);
+}
 
 #define RT_LEAF_BIT 0x80000000u
 

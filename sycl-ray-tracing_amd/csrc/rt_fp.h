@@ -17,6 +17,27 @@
 #define RT_HD inline
 #endif
 
+// Marks a loaded value as needed here (device code): the compiler then issues a
+// group of loads together and waits once, instead of sinking some of them behind
+// the first branch that reads the others (each sunk load is one more serial memory
+// round trip). No code is emitted; on the host it does nothing.
+RT_HD void rt_pin(float v)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    asm volatile("" ::"v"(v));
+#else
+    (void)v;
+#endif
+}
+RT_HD void rt_pin(int v)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    asm volatile("" ::"v"(v));
+#else
+    (void)v;
+#endif
+}
+
 RT_HD uint32_t rt_asuint(float f) { return __builtin_bit_cast(uint32_t, f); }
 RT_HD float rt_asfloat(uint32_t u) { return __builtin_bit_cast(float, u); }
 RT_HD uint64_t rt_asuint64(double d) { return __builtin_bit_cast(uint64_t, d); }

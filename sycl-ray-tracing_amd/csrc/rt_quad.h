@@ -56,15 +56,6 @@ __device__ __forceinline__ int qsum(int v)
     return v + qdpp<RT_QX2>(v);
 }
 
-// Marks loaded values as needed here: the compiler issues a record's loads together
-// and waits once, instead of sinking part of them behind the first branch that reads
-// the rest (a second, serial memory round trip per visit).
-__device__ __forceinline__ void rt_pin(float4_ v) { asm volatile("" ::"v"(v.x), "v"(v.y), "v"(v.z), "v"(v.w)); }
-__device__ __forceinline__ void rt_pin(float a, float b, float c, float d, int e)
-{
-    asm volatile("" ::"v"(a), "v"(b), "v"(c), "v"(d), "v"(e));
-}
-
 // Per-quad stack in LDS: entry i of quad q at [i * QPB + q].
 template <int N, int QPB>
 struct QuadStack {
@@ -252,7 +243,11 @@ __device__ __forceinline__ bool quad_chain_ok(const RtSceneView& S, V3 o, V3 d, 
         const float* nd = (const float*)(S.nodes + rec);  // RtNode: dn[7], df[7], ref, cnt
         const float dn0 = nd[p0], df0 = nd[7 + p0], dn1 = nd[p1 < 7 ? p1 : 0], df1 = nd[7 + (p1 < 7 ? p1 : 0)];
         const int par = S.parent[rec];
-        rt_pin(dn0, df0, dn1, df1, par);
+        rt_pin(dn0);
+        rt_pin(df0);
+        rt_pin(dn1);
+        rt_pin(df1);
+        rt_pin(par);
         float tn = -__builtin_inff(), tf = __builtin_inff();
         {
             const bool neg = r0 < 0.0;
