@@ -242,33 +242,42 @@ RT_HD float powf_(float x, float y)
 
 // ------------------------------------------------------------- sinf / cosf
 // s_sinf.c / s_cosf.c / sincosf.h (FMA build).
+// The two __sincosf_table rows share hpi_inv, hpi and the sine coefficients; the
+// cosine coefficients c0..c4 of row 1 are those of row 0 negated, and sign[] is
+// {1, -1, -1, 1} in both. The coefficients are literals here (a lane-varying row
+// index into the table would be a memory load per coefficient); negating every
+// coefficient of a chain of fma negates its correctly rounded result exactly.
+#define RT_SC_HPI_INV 0x41645f306dc9c883ull
+#define RT_SC_HPI 0x3ff921fb54442d18ull
+RT_HD double sc_sign(int n) { return ((n + 1) & 2) ? -1.0 : 1.0; }  // sign[n & 3]
+RT_HD double sc_c(uint64_t c, int tab) { return tab ? -rt_asdouble(c) : rt_asdouble(c); }
+
 RT_HD float sinf_poly_sin(double xs, double x2, int tab)
 {
-    const uint64_t* p = SINCOSF_TAB + 14 * tab;
-    const double s1 = rt_fma(x2, tabd(p, 12), tabd(p, 10));
+    (void)tab;  // (the sine coefficients are the same in both rows)
+    const double s1 = rt_fma(x2, rt_asdouble(0xbf2994eb3774cf24ull), rt_asdouble(0x3f81107605230bc4ull));
     const double x3 = x2 * xs;
     const double x5 = x3 * x2;
-    const double s = rt_fma(x3, tabd(p, 8), xs);
+    const double s = rt_fma(x3, rt_asdouble(0xbfc555545995a603ull), xs);
     return (float)rt_fma(s1, x5, s);
 }
 
 RT_HD float sinf_poly_cos(double x2, int tab)
 {
-    const uint64_t* p = SINCOSF_TAB + 14 * tab;
     const double x4 = x2 * x2;
-    const double c1 = rt_fma(x2, tabd(p, 7), tabd(p, 6));
-    const double c2 = rt_fma(x2, tabd(p, 13), tabd(p, 11));
+    const double c1 = rt_fma(x2, sc_c(0xbfdffffffd0c621cull, tab), sc_c(0x3ff0000000000000ull, tab));
+    const double c2 = rt_fma(x2, sc_c(0x3ef99343027bf8c3ull, tab), sc_c(0xbf56c087e89a359dull, tab));
     const double x6 = x4 * x2;
-    const double c = rt_fma(x4, tabd(p, 9), c1);
+    const double c = rt_fma(x4, sc_c(0x3fa55553e1068f19ull, tab), c1);
     return (float)rt_fma(c2, x6, c);
 }
 
 RT_HD double reduce_fast(double x, int* np)
 {
-    const double r = x * tabd(SINCOSF_TAB, 4);
+    const double r = x * rt_asdouble(RT_SC_HPI_INV);
     const int n = ((int32_t)r + 0x800000) >> 24;
     *np = n;
-    return rt_fma(-(double)n, tabd(SINCOSF_TAB, 5), x);
+    return rt_fma(-(double)n, rt_asdouble(RT_SC_HPI), x);
 }
 
 RT_HD double reduce_large(uint32_t xi, int* np)
@@ -301,7 +310,7 @@ RT_HD float sinf_(float y)
     if (abstop < 0x42f) {  // |y| < 120
         int n;
         const double xr = reduce_fast(x, &n);
-        const double s = tabd(SINCOSF_TAB, n & 3);
+        const double s = sc_sign(n);
         const int tab = (n & 2) ? 1 : 0;
         const double x2 = xr * xr;
         if ((n & 1) == 0) return sinf_poly_sin(xr * s, x2, tab);
@@ -311,7 +320,7 @@ RT_HD float sinf_(float y)
         const int sign = (int)(iy >> 31);
         int n;
         const double xr = reduce_large(iy, &n);
-        const double s = tabd(SINCOSF_TAB, (n + sign) & 3);
+        const double s = sc_sign(n + sign);
         const int tab = ((n + sign) & 2) ? 1 : 0;
         const double x2 = xr * xr;
         if ((n & 1) == 0) return sinf_poly_sin(xr * s, x2, tab);
@@ -332,7 +341,7 @@ RT_HD float cosf_(float y)
     if (abstop < 0x42f) {
         int n;
         const double xr = reduce_fast(x, &n);
-        const double s = tabd(SINCOSF_TAB, n & 3);
+        const double s = sc_sign(n);
         const int tab = (n & 2) ? 1 : 0;
         const double x2 = xr * xr;
         if ((n & 1) != 0) return sinf_poly_sin(xr * s, x2, tab);
@@ -342,7 +351,7 @@ RT_HD float cosf_(float y)
         const int sign = (int)(iy >> 31);
         int n;
         const double xr = reduce_large(iy, &n);
-        const double s = tabd(SINCOSF_TAB, (n + sign) & 3);
+        const double s = sc_sign(n + sign);
         const int tab = ((n + sign) & 2) ? 1 : 0;
         const double x2 = xr * xr;
         if ((n & 1) != 0) return sinf_poly_sin(xr * s, x2, tab);
