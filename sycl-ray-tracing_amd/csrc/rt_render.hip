@@ -571,6 +571,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_OC
         ps = &qs;
         const uint64_t t_chunk = __builtin_amdgcn_s_memrealtime();
 #endif
+        const unsigned long long v0 = STATS ? st.c[RT_STAT_VOL] + st.c[RT_STAT_ANY_VOL] : 0;
         if (idx < total) {
             // queue item: segment (kind, shard) of global index g
             const int g = (closest ? c0 : a0) + idx;
@@ -628,6 +629,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_OC
             }
         }
 #endif
+        if (STATS && W.iterq && idx < total && sub == 0 && W.iter < RT_MAX_TIMED_ITERS) {
+            // (RT_ITER_LOG: the longest walk of the launch in node visits, per role, and
+            // how many walks took more than 24)
+            const int nv = (int)((st.c[RT_STAT_VOL] + st.c[RT_STAT_ANY_VOL] - v0) / 4);
+            int32_t* q2 = W.iterq + 2 * RT_MAX_TIMED_ITERS + 4 * W.iter;
+            atomicMax(q2 + (closest ? 0 : 1), nv);
+            if (nv > 24) atomicAdd(q2 + 2, 1);
+        }
         const int f = wave_append(fbn, fail);
         if (fail) {
             r.d.w = rt_asfloat(target & 7u);
@@ -1084,8 +1093,8 @@ static int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounce
     if (S) HIPCHK(c, hipMemsetAsync(b->stats.p, 0, b->stats.bytes, s));
     const char* iter_log = getenv("RT_ITER_LOG");  // per-iteration log of lane 0: counts (stats renders) / ms (timed)
     if (S && iter_log) {
-        if (int r = ensure(c, b->iterq, RT_MAX_TIMED_ITERS * 8)) return r;
-        HIPCHK(c, hipMemsetAsync(b->iterq.p, 0, RT_MAX_TIMED_ITERS * 8, s));
+        if (int r = ensure(c, b->iterq, RT_MAX_TIMED_ITERS * 24)) return r;
+        HIPCHK(c, hipMemsetAsync(b->iterq.p, 0, RT_MAX_TIMED_ITERS * 24, s));
     }
     // lanes: rows interleave (row j of the launch -> lane j % lanes); pixel lists split in runs
     int nl = b->lanes;
@@ -1290,11 +1299,13 @@ static int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounce
     }
     b->tail_iter = L[0].tail_iter;
     if (S && iter_log) {
-        std::vector<int32_t> hq((size_t)2 * RT_MAX_TIMED_ITERS);
+        std::vector<int32_t> hq((size_t)6 * RT_MAX_TIMED_ITERS);
         HIPCHK(c, hipMemcpyAsync(hq.data(), b->iterq.p, hq.size() * 4, hipMemcpyDeviceToHost, s));
         HIPCHK(c, hipStreamSynchronize(s));
         if (FILE* f = fopen((std::string(iter_log) + ".counts").c_str(), "w")) {
-            for (int i = 0; i <= L[0].it && i < RT_MAX_TIMED_ITERS; i++) fprintf(f, "%d %d %d\n", i, hq[2 * i], hq[2 * i + 1]);
+            const int32_t* h2 = hq.data() + 2 * RT_MAX_TIMED_ITERS;
+            for (int i = 0; i <= L[0].it && i < RT_MAX_TIMED_ITERS; i++)
+                fprintf(f, "%d %d %d %d %d %d\n", i, hq[2 * i], hq[2 * i + 1], h2[4 * i], h2[4 * i + 1], h2[4 * i + 2]);
             fclose(f);
         }
     }
