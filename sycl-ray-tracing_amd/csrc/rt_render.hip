@@ -202,13 +202,27 @@ __device__ __forceinline__ void append_emit(const rtk::WaveView& W, int pout, in
     const int cps = ((n_in + 63) / 64 + RT_QSHARDS - 1) / RT_QSHARDS;  // chunks per shard
     const int sh = min(RT_QSHARDS - 1, (base >> 6) / cps);
     const size_t seg = (size_t)sh * W.seg_cap;
+    // the six reservations (five queues, the live list) issued back to back by lane 0
+    // and waited for once, then the stores: one atomic round trip, not six in a row
+    unsigned long long b[rtk::RK_COUNT + 1];
+#pragma unroll
+    for (int k = 0; k < rtk::RK_COUNT; k++) b[k] = __ballot((e.mask >> k) & 1u);
+    b[rtk::RK_COUNT] = __ballot(e.active);
+    int r[rtk::RK_COUNT + 1];
+    if (lane_id() == 0) {
+#pragma unroll
+        for (int k = 0; k <= rtk::RK_COUNT; k++)
+            r[k] = b[k] ? atomicAdd(W.counters + (k < rtk::RK_COUNT ? qc_at(pout, k, sh) : ac_at(pout, sh)),
+                                    __popcll(b[k]))
+                        : 0;
+    }
+    const unsigned long long lt = (lane_id() == 0) ? 0ull : (~0ull >> (64 - lane_id()));
 #pragma unroll
     for (int k = 0; k < rtk::RK_COUNT; k++) {
-        const bool want = (e.mask >> k) & 1u;
-        const int i = wave_append(W.counters + qc_at(pout, k, sh), want);
-        if (want) W.q[k][seg + i] = e.r[k];
+        const int i = __shfl(r[k], 0) + __popcll(b[k] & lt);
+        if ((e.mask >> k) & 1u) W.q[k][seg + i] = e.r[k];
     }
-    const int a = wave_append(W.counters + ac_at(pout, sh), e.active);
+    const int a = __shfl(r[rtk::RK_COUNT], 0) + __popcll(b[rtk::RK_COUNT] & lt);
     if (e.active) W.act_out[seg + a] = p;
 }
 
