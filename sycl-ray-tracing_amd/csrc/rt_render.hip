@@ -1118,7 +1118,8 @@ static int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounce
     int tail_p = 5;  // (5 paths: 15 queries, one pass of the wave's 16 quads; sweep 2-6 within 1 %)
     if (const char* e = getenv("RT_TAIL_PATHS")) tail_p = std::min(RT_TAIL_MAXP, std::max(0, atoi(e)));
     const int tail_blocks = dev_cus * RT_TAIL_OCC;  // one grid-fill of k_tail
-    const long tail_max = (long)tail_blocks * 4 * tail_p / nl;
+    long tail_max = (long)tail_blocks * 4 * tail_p / nl;  // (one grid-fill's pool per lane)
+    if (const char* e = getenv("RT_TAIL_ENTER")) tail_max = (long)(tail_max * atof(e));  // (sweeps)
     if (nl > 1) {
         HIPCHK(c, hipEventRecord(b->ev_fork, s));
         for (int l = 1; l < nl; l++) HIPCHK(c, hipStreamWaitEvent(b->ls[l], b->ev_fork, 0));
