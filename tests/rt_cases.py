@@ -81,3 +81,30 @@ def run_oracle(entry: dict, cameras: dict, threads: int = 0) -> np.ndarray:
 CORNELL_CASES = ["cfg1_cornell12", "cornell32_128", "cornell32_64spp", "mis_512"]
 DRAGON_CASES = ["cfg2_dragon", "cfg3_dragon", "cfg4_dragon4k"] + [
     f"cfg5_sweep_m{m}_r{r}" for m in range(4) for r in range(4)]
+
+
+def tiny_scene(n: int):
+    """The first n triangles of cornell12 (0: an empty scene, only the sky): the
+    degenerate octree / search-BVH shapes (no root children, one leaf, a leaf that
+    splits at the 4-triangle limit)."""
+    from conftest import parsed_scene
+    P = parsed_scene("cornell12")
+    tris = P.triangles[:n].copy() if n else np.zeros((0, 9), np.float32)
+    mi = P.material_indices[:n].copy()
+    em = np.array([i for i in P.emissive_triangle_indices if i < n], np.int32)
+    return tris, mi, P.materials, em
+
+
+def render_tiny(n: int, cameras: dict, hostsim: bool, W=24, H=20, spp=2, nb=3):
+    """(got, want): the tiny scene through the product (or hostsim) and the oracle."""
+    from oracle_bindings import OracleScene
+    tris, mi, mats, em = tiny_scene(n)
+    env = sky("S")
+    c = cameras["cornell"]
+    want, _ = OracleScene(tris, mi, mats, em, env=env).render(c, W, H, spp, nb)
+    fb = rt_amd.Image(W, H)
+    rk = rt_amd.RenderKernel(W, H, spp, nb, fb, tris, mats, em, mi, None, rt_amd.BVH(tris),
+                             rt_amd.Image.from_rgb(env), None, hostsim=hostsim)
+    rk.set_camera(rt_amd.Camera(c[:16], c[16]))
+    rk.render()
+    return fb.pixels, want

@@ -270,3 +270,12 @@ def test_gpu_schedules_bit_identical(monkeypatch):
     for off in (0, 1):
         got = render(3, 4, off, 2)
         np.testing.assert_array_equal(got.view(np.uint32), base[off::2].view(np.uint32), err_msg=f"shard {off}/2")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [0, 1, 2, 5])
+def test_gpu_tiny_scenes_match_oracle(n, cameras):
+    """Empty scene (sky only), one and two triangles, five (one leaf split):
+    the degenerate search-BVH and octree shapes through the gfx950 kernels."""
+    got, want = rt_cases.render_tiny(n, cameras, hostsim=False)
+    assert_parity(got, want, min_bitwise=1.0)

@@ -154,3 +154,10 @@ def test_hostsim_random_configs_match_oracle(scene, cam, cameras):
         rk.set_camera(rt_amd.Camera(c[:16], c[16]))
         rk.render()
         assert gio.compare_rgb(fb.pixels, want)["bitwise_fraction"] == 1.0, (W, H, spp, nb)
+
+
+@pytest.mark.parametrize("n", [0, 1, 2, 5])
+def test_hostsim_tiny_scenes_match_oracle(n, cameras):
+    """Empty scene (sky only), one and two triangles, five (one leaf split)."""
+    got, want = rt_cases.render_tiny(n, cameras, hostsim=True)
+    assert gio.compare_rgb(got, want)["bitwise_fraction"] == 1.0
