@@ -95,6 +95,36 @@ static const uint32_t INV_PIO4[24] = {
 
 RT_HD double tabd(const uint64_t* t, int i) { return rt_asdouble(t[i]); }
 
+// The expf / powf tables are indexed by a lane-varying key; in device code they are
+// read from an LDS copy (one 8-B LDS read instead of a global load per lookup, each
+// on the dependent chain of a powf). Every kernel that evaluates expf / exp2 / powf
+// fills the copy first with lds_tables_init() (k_init, k_step, k_tail, k_libm).
+#if defined(__HIPCC__)
+__shared__ uint64_t rt_libm_lds[64];  // [0, 32) POWF_LOG2_TAB, [32, 64) EXP2F_TAB
+__device__ __forceinline__ void lds_tables_init()
+{
+    for (int i = (int)threadIdx.x; i < 64; i += (int)blockDim.x)
+        rt_libm_lds[i] = i < 32 ? POWF_LOG2_TAB[i] : EXP2F_TAB[i - 32];
+    __syncthreads();
+}
+#endif
+RT_HD uint64_t exp2_tab(uint64_t i)  // EXP2F_TAB[i], i < 32
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    return rt_libm_lds[32 + i];
+#else
+    return EXP2F_TAB[i];
+#endif
+}
+RT_HD double log2_tab(int i)  // POWF_LOG2_TAB[i] as a double
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    return rt_asdouble(rt_libm_lds[i]);
+#else
+    return rt_asdouble(POWF_LOG2_TAB[i]);
+#endif
+}
+
 // __math_oflowf / __math_uflowf / __math_may_uflowf / __math_invalidf results
 // (sysdeps/ieee754/flt-32/math_errf.c) under round-to-nearest.
 RT_HD float oflowf(uint32_t sign) { return sign ? -__builtin_inff() : __builtin_inff(); }
@@ -123,7 +153,7 @@ RT_HD float expf_(float x)
     const uint64_t ki = rt_asuint64(kd);
     kd -= SHIFT;
     const double r = rt_fma(InvLn2N, xd, -kd);
-    uint64_t t = EXP2F_TAB[ki % 32];
+    uint64_t t = exp2_tab(ki % 32);
     t += ki << 47;
     const double s = rt_asdouble(t);
     const double z = rt_fma(0x1.c6af84b912394p-20, r, 0x1.ebfce50fac4f3p-13);
@@ -159,8 +189,8 @@ RT_HD double log2_inline(uint32_t ix)
     const uint32_t top = tmp & 0xff800000u;
     const uint32_t iz = ix - top;
     const int k = (int32_t)top >> 23;
-    const double invc = tabd(POWF_LOG2_TAB, 2 * i);
-    const double logc = tabd(POWF_LOG2_TAB, 2 * i + 1);
+    const double invc = log2_tab(2 * i);
+    const double logc = log2_tab(2 * i + 1);
     const double z = (double)rt_asfloat(iz);
     const double r = rt_fma(z, invc, -1.0);
     const double y0 = logc + (double)k;
@@ -181,7 +211,7 @@ RT_HD float exp2_inline(double xd, uint32_t sign_bias)
     const uint64_t ki = rt_asuint64(kd);
     kd -= SHIFT;
     const double r = xd - kd;
-    uint64_t t = EXP2F_TAB[ki % 32];
+    uint64_t t = exp2_tab(ki % 32);
     const uint64_t ski = ki + sign_bias;
     t += ski << 47;
     const double s = rt_asdouble(t);

@@ -272,6 +272,7 @@ __device__ __forceinline__ int shard_find(const int* pre, int m, int g)
 // Path init: every slot seeds its RNG and emits its first camera ray (into Q[0], ACT[0]).
 __global__ __launch_bounds__(256) void k_init(rtk::WaveView W)
 {
+    rtlibm::lds_tables_init();  // (a pixel of a 0-bounce render is tone-mapped here)
     const int p = blockIdx.x * blockDim.x + threadIdx.x;  // grid covers whole waves
     rtk::Emit e;
     e.mask = 0;
@@ -476,6 +477,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_STEP_OCC
 {
     __shared__ uint32_t s_lds[RT_LDS_WORDS * 256];
     __shared__ int s_pre[RT_QSHARDS + 1];
+    rtlibm::lds_tables_init();
     int32_t* cnt = W.counters;
     if (blockIdx.x == 0 && threadIdx.x == 0) {  // for k_trace(i + 1); DONE[par ^ 1] was released by k_trace(i)
         cnt[C_FBC0 + (par ^ 1)] = cnt[C_FBA0 + (par ^ 1)] = 0;
@@ -687,6 +689,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TAIL_OCC
     __shared__ rtk::RayRec s_q[4][2][RT_TAIL_MAXP * rtk::RK_COUNT];  // per wave: closest list, occlusion list
     __shared__ uint32_t s_stk[2 * RT_QSTACK * 64];
     __shared__ int s_pre[RT_QSHARDS + 1];
+    rtlibm::lds_tables_init();
     int32_t* cnt = W.counters;
     shard_prefix(cnt, RT_QSHARDS, [&](int j) { return ac_at(par, j); }, s_pre);
     const int n = s_pre[RT_QSHARDS];
@@ -937,6 +940,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
 // numerics self-test kernel (tests/test_gpu_parity.py): out[i] = f(in[i])
 __global__ void k_libm(int fn, const float* __restrict__ in, const float* __restrict__ in2, float* __restrict__ out, int n)
 {
+    rtlibm::lds_tables_init();
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const float x = in[i];
