@@ -104,6 +104,8 @@ struct Backend {
     DevBuf fb;        // host-fb staging
     int32_t* h_act[RT_MAX_LANES] = {};     // per lane, pinned: live-slot counters (sharded) + 8 fallback counters
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    hipEvent_t ev_done = nullptr;  // end of the last run_wave (all lanes joined): the next render waits for it
+    bool done_recorded = false;
     hipStream_t ls[RT_MAX_LANES] = {};      // lanes 1.. streams (lane 0 runs on the caller's)
     hipEvent_t ev_fork = nullptr, ev_join[RT_MAX_LANES] = {}, ev_lane[RT_MAX_LANES] = {};
     int lanes = 3;                          // RT_LANES (sweep on cfg2: 452 / 499 / 519 / 509 Msamples/s for 1-4)
@@ -491,6 +493,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_STEP_OCC
     // spill lanes and a quarter of the grid each
     const int nrc = min(cnt[C_PARKC0 + (par ^ 1)], W.park_cap), nra = min(cnt[C_PARKA0 + (par ^ 1)], W.park_cap);
     const int ec = nrc + cnt[C_FBC0 + par], ea = nra + cnt[C_FBA0 + par];
+    // (the host launches >= 3 blocks, so both exact roles and the path step each get one:
+    // with gridDim 3, half = 1; above, the exact roles take at most half of the grid)
     const int half = min(W.spill_lanes / 512, max(1, (int)gridDim.x / 4));
     const int nbe_c = min(half, (ec + 63) / 64), nbe_a = min(half, (ea + 63) / 64);
     const int b = (int)blockIdx.x;
@@ -984,6 +988,7 @@ int rt_backend_create(rt_context* c)
         if (l > 0) HIPCHK(c, hipStreamCreateWithFlags(&b->ls[l], hipStreamNonBlocking));
     }
     HIPCHK(c, hipEventCreateWithFlags(&b->ev_fork, hipEventDisableTiming));
+    HIPCHK(c, hipEventCreateWithFlags(&b->ev_done, hipEventDisableTiming));
     if (const char* e = getenv("RT_LANES")) b->lanes = std::min(RT_MAX_LANES, std::max(1, atoi(e)));
     if (const char* e = getenv("RT_STEP_BUDGET")) b->budget = std::max(1, atoi(e));
     return RT_OK;
@@ -1009,6 +1014,7 @@ void rt_backend_destroy(rt_context* c)
         if (b->ls[l]) (void)hipStreamDestroy(b->ls[l]);
     }
     if (b->ev_fork) (void)hipEventDestroy(b->ev_fork);
+    if (b->ev_done) (void)hipEventDestroy(b->ev_done);
     for (auto& lane : b->tev)
         for (auto& row : lane)
         for (hipEvent_t ev : row)
@@ -1100,6 +1106,9 @@ static int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounce
                     float4_* fb, hipStream_t s)
 {
     if (n <= 0) return RT_OK;
+    // every render of a context reuses its lanes' slots and counters: the previous render
+    // (whose tail kernel may still run, on another stream) must finish first
+    if (b->done_recorded) HIPCHK(c, hipStreamWaitEvent(s, b->ev_done, 0));
     int dev_cus = 256;
     (void)hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, c->device);
     const int threads = 256;
@@ -1199,8 +1208,10 @@ static int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounce
     // grids sized by the last known live count: k_step one slot per thread; k_trace up to
     // five queries per path, a quad each, over two grid-fills, never fewer blocks than the
     // exact-walk roles can claim (dev_cus * 4) plus room for the fast roles
+    // (k_step: at least 3 blocks, one per exact-walk role and one for the path step, so a
+    // small live count with fallbacks or parked walks pending still steps its paths)
     auto step_blocks_of = [&](const WaveLane& La) {
-        return (int)std::max(1l, std::min((La.live + threads - 1) / threads, (long)dev_cus * 8));
+        return (int)std::max(3l, std::min((La.live + threads - 1) / threads, (long)dev_cus * 8));
     };
     auto trace_blocks_of = [&](const WaveLane& La) {
         const long want = (20 * La.live + 2 * threads - 1) / (2 * threads);
@@ -1317,6 +1328,8 @@ static int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounce
         }
     }
     b->tail_iter = L[0].tail_iter;
+    HIPCHK(c, hipEventRecord(b->ev_done, s));
+    b->done_recorded = true;
     if (S && iter_log) {
         std::vector<int32_t> hq((size_t)6 * RT_MAX_TIMED_ITERS);
         HIPCHK(c, hipMemcpyAsync(hq.data(), b->iterq.p, hq.size() * 4, hipMemcpyDeviceToHost, s));

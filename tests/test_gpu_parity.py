@@ -279,3 +279,26 @@ def test_gpu_tiny_scenes_match_oracle(n, cameras):
     the degenerate search-BVH and octree shapes through the gfx950 kernels."""
     got, want = rt_cases.render_tiny(n, cameras, hostsim=False)
     assert_parity(got, want, min_bitwise=1.0)
+
+
+@pytest.mark.parametrize("name", ["mis_512", "cfg2_dragon", "cornell32_128"])
+def test_gpu_parked_walks_small_launches(name, manifest, cameras, monkeypatch):
+    """Exact-walk hand-off under stress: a step budget of 1 parks
+    every exact walk at its first node boundary, and with the tail kernel off
+    the last iterations run k_step on a live count of a few paths, where the
+    grid is smallest while fallbacks and parked walks are still pending. Every
+    pixel must still be written, bit for bit the reference's."""
+    monkeypatch.setenv("RT_STEP_BUDGET", "1")
+    monkeypatch.setenv("RT_TAIL_PATHS", "0")
+    e = rt_cases.golden_case(name, manifest)
+    rk, fb = rt_cases.make_kernel(e, cameras, hostsim=False)
+    rk.set_stats(True)
+    if e.get("px") is None:
+        rk.render()
+        got = fb.pixels
+    else:
+        rk.ray_trace_pixels(e["px"])
+        got = fb.pixels[e["px"][:, 1], e["px"][:, 0]]
+    st = rk.stats()
+    print(name, "fallbacks", st["fallback"], "iterations", rk.last_iterations())
+    assert_parity(got, e["expected"], min_bitwise=1.0)
