@@ -48,6 +48,17 @@ typedef struct rt_mesh rt_mesh;
 
 /* ---------------------------------------------------------------- context */
 int rt_create(int device, rt_context** out);
+/* One context over n_devices GPUs of this process (devices[] = HIP ordinals,
+ * NULL = 0..n-1; devices[0] is the root). Scene, BVH and env are replicated on
+ * every device; a render shards the frame's rows (row j of the request ->
+ * device j mod n), ncclScatter's the root framebuffer's rows to their devices,
+ * renders every shard on its own device and ncclGather's them back to the root
+ * (single-process RCCL clique, ncclCommInitAll). The result is bit-identical to
+ * a single-device render. Replaces the OpenMP row loop of RenderKernel::render
+ * (render_kernel.cpp:189-211) for a whole node. RT_ERR_NODEV if a device or
+ * librccl.so.1 is missing. */
+int rt_create_multi(int n_devices, const int* devices, rt_context** out);
+int rt_device_count(const rt_context* ctx);
 void rt_destroy(rt_context* ctx);
 const char* rt_last_error(const rt_context* ctx); /* ctx may be NULL: last global error */
 int rt_version(void);
@@ -56,6 +67,13 @@ int rt_version(void);
 int rt_set_scene(rt_context* ctx, const float* triangles, int n_triangles, const int* material_indices,
                  int n_material_indices, const float* materials, int n_materials, const int* emissive_triangles,
                  int n_emissive, const float* spheres, int n_spheres);
+
+/* The material buffer alone, for a context whose scene is set: the reference
+ * keeps `const std::vector<SimpleMaterial>&` (render_kernel.h:81-93), so a
+ * caller may edit materials between render() calls (the cfg5 material sweep);
+ * this pushes the new table without rebuilding the octree / search BVH.
+ * Material indices must stay in range. */
+int rt_set_materials(rt_context* ctx, const float* materials, int n_materials);
 
 /* BVH(&triangles, max_depth, leaf_max_obj_count): native octree build,
  * bit-identical to bvh.h:55-125 (child-box quirk included). */
@@ -84,7 +102,8 @@ int rt_render(rt_context* ctx, int width, int height, int samples, int max_bounc
 
 /* Device-resident render for benchmarking / multi-GPU sharding: renders image
  * rows y = row_offset + j*row_stride (j = 0..) into d_fb (device, rows_local*w*4
- * floats, row j of the shard at offset j*w*4). stream may be NULL (default). */
+ * floats, row j of the shard at offset j*w*4). stream may be NULL (default).
+ * Multi-device context: d_fb and stream live on the root device. */
 int rt_render_device(rt_context* ctx, int width, int height, int samples, int max_bounces, void* d_fb,
                      int row_offset, int row_stride, void* stream);
 

@@ -19,7 +19,10 @@ void set_global_err(const std::string& m)
 
 int rt_fail(rt_context* ctx, int code, const std::string& msg)
 {
-    if (ctx) ctx->err = msg;
+    if (ctx) {  // (a multi-device render fails from its device threads)
+        std::lock_guard<std::mutex> lk(g_err_mu);
+        ctx->err = msg;
+    }
     set_global_err(msg);
     return code;
 }
@@ -86,12 +89,34 @@ int rt_create(int device, rt_context** out)
     int r = rt_backend_create(c);
     if (r) {
         set_global_err(c->err);
+        rt_backend_destroy(c);
         delete c;
         return r;
     }
     *out = c;
     return RT_OK;
 }
+
+int rt_create_multi(int n_devices, const int* devices, rt_context** out)
+{
+    if (!out) return rt_fail(nullptr, RT_ERR_ARG, "rt_create_multi: out is NULL");
+    *out = nullptr;
+    if (n_devices < 1 || n_devices > 64) return rt_fail(nullptr, RT_ERR_ARG, "rt_create_multi: n_devices must be 1..64");
+    rt_context* c = new rt_context();
+    for (int d = 0; d < n_devices; d++) c->devices.push_back(devices ? devices[d] : d);
+    c->device = c->devices[0];
+    int r = rt_backend_create(c);
+    if (r) {
+        set_global_err(c->err);
+        rt_backend_destroy(c);
+        delete c;
+        return r;
+    }
+    *out = c;
+    return RT_OK;
+}
+
+int rt_device_count(const rt_context* ctx) { return ctx ? (ctx->devices.empty() ? 1 : (int)ctx->devices.size()) : RT_ERR_ARG; }
 
 void rt_destroy(rt_context* ctx)
 {
@@ -137,6 +162,21 @@ int rt_set_scene(rt_context* c, const float* triangles, int n, const int* materi
     c->have_scene = true;
     c->have_bvh = false;
     c->dirty = true;
+    return RT_OK;
+}
+
+int rt_set_materials(rt_context* c, const float* materials, int n_mats)
+{
+    if (!c || !c->have_scene) return rt_fail(c, RT_ERR_STATE, "rt_set_materials: no scene");
+    if (n_mats <= 0 || !materials) return rt_fail(c, RT_ERR_ARG, "rt_set_materials: bad buffer");
+    for (int32_t mi : c->mat_idx)
+        if (mi >= n_mats) return rt_fail(c, RT_ERR_ARG, "rt_set_materials: a material index is out of range");
+    c->mats.resize(n_mats);
+    for (int i = 0; i < n_mats; i++) {
+        const float* p = materials + 10 * (size_t)i;
+        c->mats[i] = RtMat{p[0], p[1], p[2], p[8], p[4], p[5], p[6], p[9]};
+    }
+    c->mats_dirty_only = true;  // the octree, search BVH, triangles and env stay on the device
     return RT_OK;
 }
 
@@ -240,10 +280,11 @@ static int check_ready(rt_context* c, int w, int h, int spp, int bounces)
     // the reference seeds with the int 31 + x*y*spp (render_kernel.cpp:77)
     if ((double)(w - 1) * (double)(h - 1) * (double)spp + 31.0 > 2147483647.0)
         return rt_fail(c, RT_ERR_ARG, "31 + x*y*spp overflows int (reference seed)");
-    if (c->dirty) {
+    if (c->dirty || c->mats_dirty_only) {
         int r = rt_backend_upload(c);
         if (r) return r;
         c->dirty = false;
+        c->mats_dirty_only = false;
     }
     return RT_OK;
 }
@@ -289,6 +330,7 @@ int rt_intersect(rt_context* c, const float* rays, int n, void* out)
         int r = rt_backend_upload(c);
         if (r) return r;
         c->dirty = false;
+        c->mats_dirty_only = false;
     }
     return rt_backend_intersect(c, rays, n, out);
 }

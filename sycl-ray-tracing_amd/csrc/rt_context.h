@@ -14,6 +14,9 @@
 
 struct rt_context {
     int device = 0;
+    // rt_create_multi: the devices a render shards over (rows y -> device y mod N, RCCL
+    // scatter / gather through devices[0]); empty for a single-device context (rt_create)
+    std::vector<int> devices;
     std::string err;
 
     // RenderKernel constructor inputs (render_kernel.h:27-34)
@@ -45,6 +48,7 @@ struct rt_context {
     double last_kernel_ms = 0.0;
 
     bool dirty = true;            // host state changed since the last upload
+    bool mats_dirty_only = false; // only the material table changed (rt_set_materials)
     void* backend = nullptr;
 };
 

@@ -234,6 +234,34 @@ static int run_wave_host(rt_context* c, int w, int h, int spp, int bounces, cons
     return RT_OK;
 }
 
+// A compacted shard (row j = image row off + j*stride). A multi-device context
+// (rt_create_multi) splits it the way the gfx950 backend's render_multi does: row j to
+// "device" j mod N, each device's rows packed into a block, rendered as the rows
+// off + d*stride + k*N*stride, and un-permuted (here with host copies instead of
+// ncclScatter / ncclGather).
+static int render_shard(rt_context* c, int w, int h, int spp, int bounces, int off, int stride, int rows,
+                        float4_* shard)
+{
+    const int N = c->devices.empty() ? 1 : (int)c->devices.size();
+    if (N == 1) {
+        rtk::PixSrc src{w, off, stride, nullptr};
+        return run_wave_host(c, w, h, spp, bounces, src, rows * w, shard);
+    }
+    std::vector<rtk::Stats> sum(1);
+    std::memset(&sum[0], 0, sizeof sum[0]);
+    for (int d = 0; d < N; d++) {
+        const int rows_d = rows > d ? (rows - d + N - 1) / N : 0;
+        std::vector<float4_> blk((size_t)rows_d * w);
+        for (int k = 0; k < rows_d; k++) std::memcpy(&blk[(size_t)k * w], shard + (size_t)(d + k * N) * w, 16 * (size_t)w);
+        rtk::PixSrc src{w, off + d * stride, N * stride, nullptr};
+        if (int r = run_wave_host(c, w, h, spp, bounces, src, rows_d * w, blk.data())) return r;
+        for (int k = 0; k < rows_d; k++) std::memcpy(shard + (size_t)(d + k * N) * w, &blk[(size_t)k * w], 16 * (size_t)w);
+        for (int i = 0; i < RT_STAT_COUNT; i++) sum[0].c[i] += rows_d ? c->stats[i] : 0;
+    }
+    merge_stats(c, sum);
+    return RT_OK;
+}
+
 int rt_backend_render(rt_context* c, int w, int h, int spp, int bounces, float* host_fb, void* dev_fb, int row_offset,
                       int row_stride, void*)
 {
@@ -242,18 +270,17 @@ int rt_backend_render(rt_context* c, int w, int h, int spp, int bounces, float* 
     // j*row_stride (rt_render_device semantics, used by the gloo tests).
     const int rows_local = (h - row_offset + row_stride - 1) / row_stride;
     const double t0 = omp_get_wtime();
-    rtk::PixSrc src{w, row_offset, row_stride, nullptr};
     int r;
     if (host_fb) {
         // the full frame holds all rows; the wavefront works on the shard's rows
         std::vector<float4_> shard((size_t)rows_local * w);
         for (int j = 0; j < rows_local; j++)
             std::memcpy(&shard[(size_t)j * w], host_fb + 4 * (size_t)(row_offset + j * row_stride) * w, 16 * (size_t)w);
-        r = run_wave_host(c, w, h, spp, bounces, src, rows_local * w, shard.data());
+        r = render_shard(c, w, h, spp, bounces, row_offset, row_stride, rows_local, shard.data());
         for (int j = 0; j < rows_local; j++)
             std::memcpy(host_fb + 4 * (size_t)(row_offset + j * row_stride) * w, &shard[(size_t)j * w], 16 * (size_t)w);
     } else {
-        r = run_wave_host(c, w, h, spp, bounces, src, rows_local * w, (float4_*)dev_fb);
+        r = render_shard(c, w, h, spp, bounces, row_offset, row_stride, rows_local, (float4_*)dev_fb);
     }
     c->last_kernel_ms = (omp_get_wtime() - t0) * 1e3;
     return r;

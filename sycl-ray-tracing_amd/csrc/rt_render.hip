@@ -23,6 +23,12 @@
 #include <vector>
 #include <algorithm>
 
+#include <dlfcn.h>
+#include <mutex>
+#include <thread>
+
+#include <rccl/rccl.h>
+
 #include "rt_context.h"
 #include "rt_wave.h"
 #include "rt_quad.h"
@@ -94,6 +100,8 @@ __host__ __device__ __forceinline__ int ac_at(int par, int shard)
 }
 
 struct Backend {
+    int device = 0;
+    hipStream_t own = nullptr;  // device-side work not on a caller's stream (multi-device shards, pixel lists)
     DevBuf nodes, tri4, prim2k, mat_idx, mats, emissive, spheres, env, env_lum, cdf;
     DevBuf bvh4, bvh_tri4, parent, leaf_of, cdf_row, cdf_coarse, cdf_fence, matk;
     DevBuf stats;     // 2 x RT_STAT_COUNT u64: all kernels, then the tail kernel's share
@@ -142,7 +150,6 @@ int upload(rt_context* c, DevBuf& b, const std::vector<T>& v)
     return RT_OK;
 }
 
-Backend* be(rt_context* c) { return (Backend*)c->backend; }
 
 // ------------------------------------------------------------ wave helpers
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
@@ -334,6 +341,12 @@ struct FastStack {
         }
     }
 };
+
+// RT_FORCE_FALLBACK: does this query skip the quad walk (a schedule-independent hash of the ray)?
+__device__ __forceinline__ bool forced_fallback(const rtk::WaveView& W, const float4_& o, const float4_& d)
+{
+    return W.force_fb > 0 && ((rt_asuint(o.x) ^ rt_asuint(d.y) ^ (rt_asuint(d.z) >> 7)) % (uint32_t)W.force_fb) == 0u;
+}
 
 // Blocks [0, n0) take role 0, the rest role 1, in proportion to the work.
 __device__ __forceinline__ int split_blocks(int nb, int w0, int w1)
@@ -603,7 +616,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_OC
             for (int k2 = 1; k2 < rtk::RK_COUNT; k2++) qk = kind == k2 ? W.q[k2] : qk;
             r = qk[(size_t)(seg % RT_QSHARDS) * W.seg_cap + (g - s_pre[seg])];
             target = (rt_asuint(r.o.w) << 3) | (uint32_t)kind;
-            if (closest) {
+            if (forced_fallback(W, r.o, r.d)) {
+                fail = sub == 0;
+            } else if (closest) {
                 float t;
                 int k;
                 if (rtk::quad_query_closest(W.S, rtk::v3of(r.o), rtk::v3of(r.d), stk, sub, t, k, ps)) {
@@ -774,7 +789,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TAIL_OCC
                 const uint32_t target = rt_asuint(r.d.w);
                 const rtk::V3 o = rtk::v3of(r.o), d = rtk::v3of(r.d);
                 rtk::QWalk qw;
-                const int a = rtk::quad_query_mixed(W.S, o, d, stk, sub, l == 1, qw, ps);
+                const int a = forced_fallback(W, r.o, r.d) ? -1 : rtk::quad_query_mixed(W.S, o, d, stk, sub, l == 1, qw, ps);
                 if (a >= 0 && sub == 0) {
                     if (l == 0)
                         rtk::finish_closest(W, target, o, d, qw.t, qw.k);
@@ -969,16 +984,80 @@ __global__ void k_libm(int fn, const float* __restrict__ in, const float* __rest
 }  // namespace
 
 // ------------------------------------------------------------------- hooks
-int rt_backend_create(rt_context* c)
+namespace {
+// A context drives one Backend per device. rt_create: one device, renders on the
+// caller's stream. rt_create_multi: devices[0] is the root that holds the caller's
+// framebuffer; a render shards its rows over the devices (render_multi).
+struct Group {
+    std::vector<Backend*> dev;     // dev[0]: the root
+    bool multi = false;            // rt_create_multi (even with one device: the RCCL path)
+    std::vector<ncclComm_t> comms; // ncclCommInitAll over the devices, in order
+    DevBuf stage;                  // root: N blocks of rows_max rows (scatter source / gather target)
+    std::vector<DevBuf> shard;     // device d >= 1: its block
+};
+
+Group* grp(rt_context* c) { return (Group*)c->backend; }
+Backend* be(rt_context* c) { return grp(c)->dev[0]; }
+
+// RCCL, loaded on the first multi-device context: the library need not be present
+// (or be the same build as a framework's own copy) for single-device use.
+struct Rccl {
+    void* h = nullptr;
+    decltype(&ncclCommInitAll) init = nullptr;
+    decltype(&ncclCommDestroy) destroy = nullptr;
+    decltype(&ncclScatter) scatter = nullptr;
+    decltype(&ncclGather) gather = nullptr;
+    decltype(&ncclGroupStart) group_start = nullptr;
+    decltype(&ncclGroupEnd) group_end = nullptr;
+    decltype(&ncclGetErrorString) errstr = nullptr;
+};
+std::mutex g_rccl_mu;
+Rccl g_rccl;
+
+const Rccl* rccl_load(std::string& err)
+{
+    std::lock_guard<std::mutex> lk(g_rccl_mu);
+    if (g_rccl.h) return &g_rccl;
+    void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+    if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+    if (!h) {
+        err = std::string("librt_hip: RCCL not found (librccl.so.1): ") + dlerror();
+        return nullptr;
+    }
+    Rccl r;
+    r.h = h;
+    r.init = (decltype(r.init))dlsym(h, "ncclCommInitAll");
+    r.destroy = (decltype(r.destroy))dlsym(h, "ncclCommDestroy");
+    r.scatter = (decltype(r.scatter))dlsym(h, "ncclScatter");
+    r.gather = (decltype(r.gather))dlsym(h, "ncclGather");
+    r.group_start = (decltype(r.group_start))dlsym(h, "ncclGroupStart");
+    r.group_end = (decltype(r.group_end))dlsym(h, "ncclGroupEnd");
+    r.errstr = (decltype(r.errstr))dlsym(h, "ncclGetErrorString");
+    if (!r.init || !r.destroy || !r.scatter || !r.gather || !r.group_start || !r.group_end || !r.errstr) {
+        err = "librt_hip: librccl.so.1 lacks ncclCommInitAll / ncclScatter / ncclGather";
+        return nullptr;
+    }
+    g_rccl = r;
+    return &g_rccl;
+}
+
+#define NCCLCHK(ctx, R, expr)                                                                    \
+    do {                                                                                         \
+        ncclResult_t e_ = (expr);                                                                \
+        if (e_ != ncclSuccess) return rt_fail(ctx, RT_ERR_HIP, std::string(#expr ": ") + (R)->errstr(e_)); \
+    } while (0)
+
+int create_one(rt_context* c, int device, Backend** out)
 {
     int n = 0;
     hipError_t e = hipGetDeviceCount(&n);
     if (e != hipSuccess || n == 0)
         return rt_fail(c, RT_ERR_NODEV, "librt_hip: no HIP device available (this library has no CPU path)");
-    if (c->device < 0 || c->device >= n) return rt_fail(c, RT_ERR_NODEV, "librt_hip: device index out of range");
-    HIPCHK(c, hipSetDevice(c->device));
+    if (device < 0 || device >= n) return rt_fail(c, RT_ERR_NODEV, "librt_hip: device index out of range");
+    HIPCHK(c, hipSetDevice(device));
     Backend* b = new Backend();
-    c->backend = b;
+    *out = b;
+    b->device = device;
     HIPCHK(c, hipEventCreate(&b->ev0));
     HIPCHK(c, hipEventCreate(&b->ev1));
     for (int l = 0; l < RT_MAX_LANES; l++) {
@@ -987,6 +1066,7 @@ int rt_backend_create(rt_context* c)
         HIPCHK(c, hipEventCreateWithFlags(&b->ev_join[l], hipEventDisableTiming));
         if (l > 0) HIPCHK(c, hipStreamCreateWithFlags(&b->ls[l], hipStreamNonBlocking));
     }
+    HIPCHK(c, hipStreamCreateWithFlags(&b->own, hipStreamNonBlocking));
     HIPCHK(c, hipEventCreateWithFlags(&b->ev_fork, hipEventDisableTiming));
     HIPCHK(c, hipEventCreateWithFlags(&b->ev_done, hipEventDisableTiming));
     if (const char* e = getenv("RT_LANES")) b->lanes = std::min(RT_MAX_LANES, std::max(1, atoi(e)));
@@ -994,14 +1074,13 @@ int rt_backend_create(rt_context* c)
     return RT_OK;
 }
 
-void rt_backend_destroy(rt_context* c)
+void destroy_one(Backend* b)
 {
-    Backend* b = be(c);
-    if (!b) return;
-    (void)hipSetDevice(c->device);
+    (void)hipSetDevice(b->device);
+    (void)hipDeviceSynchronize();
     DevBuf* all[] = {&b->nodes, &b->tri4, &b->prim2k, &b->mat_idx, &b->mats, &b->emissive, &b->spheres, &b->env,
                      &b->env_lum, &b->cdf, &b->bvh4, &b->bvh_tri4, &b->parent, &b->leaf_of, &b->cdf_row, &b->cdf_coarse,
-                     &b->cdf_fence, &b->matk, &b->stats, &b->xy, &b->fb};
+                     &b->cdf_fence, &b->matk, &b->stats, &b->xy, &b->fb, &b->iterq};
     for (DevBuf* d : all)
         if (d->p) (void)hipFree(d->p);
     for (int l = 0; l < RT_MAX_LANES; l++)
@@ -1013,30 +1092,29 @@ void rt_backend_destroy(rt_context* c)
         if (b->ev_join[l]) (void)hipEventDestroy(b->ev_join[l]);
         if (b->ls[l]) (void)hipStreamDestroy(b->ls[l]);
     }
+    if (b->own) (void)hipStreamDestroy(b->own);
     if (b->ev_fork) (void)hipEventDestroy(b->ev_fork);
     if (b->ev_done) (void)hipEventDestroy(b->ev_done);
     for (auto& lane : b->tev)
         for (auto& row : lane)
-        for (hipEvent_t ev : row)
-            if (ev) (void)hipEventDestroy(ev);
+            for (hipEvent_t ev : row)
+                if (ev) (void)hipEventDestroy(ev);
     if (b->ev0) (void)hipEventDestroy(b->ev0);
     if (b->ev1) (void)hipEventDestroy(b->ev1);
     delete b;
-    c->backend = nullptr;
 }
 
-int rt_backend_upload(rt_context* c)
+// Scene, BVH and env of the context into one device's memory (replicated per device).
+int upload_one(rt_context* c, Backend* b, const std::vector<int32_t>& matk, bool mats_only)
 {
-    Backend* b = be(c);
-    HIPCHK(c, hipSetDevice(c->device));
-    // material index of each leaf-order triangle k: mat_idx[prim(k)] (rt_trace.h load_mat_hit)
-    std::vector<int32_t> matk(c->flat.tri4.size() / 3);
-    for (size_t k = 0; k < matk.size(); k++) {
-        int32_t prim;
-        std::memcpy(&prim, &c->flat.tri4[3 * k].w, 4);
-        matk[k] = c->mat_idx[prim];
-    }
+    HIPCHK(c, hipSetDevice(b->device));
     int r = 0;
+    if (mats_only) {  // rt_set_materials: the material table (and what depends on it) alone
+        if ((r = upload(c, b->mats, c->mats))) return r;
+        b->view.mats = (const RtMat*)b->mats.p;
+        b->bl_rays = rt_scene_has_emissive_prim(c) ? 1 : 0;
+        return RT_OK;
+    }
     if ((r = upload(c, b->nodes, c->flat.nodes)) || (r = upload(c, b->tri4, c->flat.tri4)) ||
         (r = upload(c, b->prim2k, c->flat.prim2k)) || (r = upload(c, b->mat_idx, c->mat_idx)) ||
         (r = upload(c, b->mats, c->mats)) || (r = upload(c, b->emissive, c->emissive)) ||
@@ -1082,7 +1160,75 @@ int rt_backend_upload(rt_context* c)
     b->any_rays = v.n_spheres == 0 ? 1 : 0;
     return RT_OK;
 }
+}  // namespace
 
+int rt_backend_create(rt_context* c)
+{
+    Group* g = new Group();
+    c->backend = g;
+    g->multi = !c->devices.empty();
+    const std::vector<int> ids = g->multi ? c->devices : std::vector<int>{c->device};
+    for (int d : ids) {
+        Backend* b = nullptr;
+        const int r = create_one(c, d, &b);
+        if (b) g->dev.push_back(b);
+        if (r) return r;
+    }
+    if (g->multi) {
+        std::string err;
+        const Rccl* R = rccl_load(err);
+        if (!R) return rt_fail(c, RT_ERR_NODEV, err);
+        g->comms.resize(ids.size());
+        NCCLCHK(c, R, R->init(g->comms.data(), (int)ids.size(), ids.data()));
+        g->shard.resize(ids.size());
+    }
+    return RT_OK;
+}
+
+void rt_backend_destroy(rt_context* c)
+{
+    Group* g = grp(c);
+    if (!g) return;
+    for (Backend* b : g->dev) destroy_one(b);
+    if (!g->comms.empty()) {
+        std::string err;
+        if (const Rccl* R = rccl_load(err))
+            for (ncclComm_t cm : g->comms)
+                if (cm) (void)R->destroy(cm);
+    }
+    for (size_t d = 0; d < g->shard.size(); d++)
+        if (g->shard[d].p) {
+            (void)hipSetDevice(g->multi ? c->devices[d] : c->device);
+            (void)hipFree(g->shard[d].p);
+        }
+    if (g->stage.p) {
+        (void)hipSetDevice(g->multi ? c->devices[0] : c->device);
+        (void)hipFree(g->stage.p);
+    }
+    delete g;
+    c->backend = nullptr;
+}
+
+int rt_backend_upload(rt_context* c)
+{
+    Group* g = grp(c);
+    const bool mats_only = c->mats_dirty_only && !c->dirty;
+    // material index of each leaf-order triangle k: mat_idx[prim(k)] (rt_trace.h load_mat_hit)
+    std::vector<int32_t> matk;
+    if (!mats_only) {
+        matk.resize(c->flat.tri4.size() / 3);
+        for (size_t k = 0; k < matk.size(); k++) {
+            int32_t prim;
+            std::memcpy(&prim, &c->flat.tri4[3 * k].w, 4);
+            matk[k] = c->mat_idx[prim];
+        }
+    }
+    for (Backend* b : g->dev)
+        if (int r = upload_one(c, b, matk, mats_only)) return r;
+    return RT_OK;
+}
+
+namespace {
 // One wavefront run over a subset of the launch's pixels (a "lane"): its own
 // path slots, queues, counters and stream. run_wave drives RT_LANES lanes on
 // as many streams (row j of the launch -> lane j % lanes) so that one lane's
@@ -1102,7 +1248,7 @@ struct WaveLane {
 };
 
 // Runs the wavefront loop for n slots of `src` into fb (device, n float4).
-static int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounces, const rtk::PixSrc& src, int n,
+int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounces, const rtk::PixSrc& src, int n,
                     float4_* fb, hipStream_t s)
 {
     if (n <= 0) return RT_OK;
@@ -1110,7 +1256,7 @@ static int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounce
     // (whose tail kernel may still run, on another stream) must finish first
     if (b->done_recorded) HIPCHK(c, hipStreamWaitEvent(s, b->ev_done, 0));
     int dev_cus = 256;
-    (void)hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, c->device);
+    (void)hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, b->device);
     const int threads = 256;
     // k_trace: wave-strided over 2 grid-fills; RT_TRACE_OCC blocks resident per CU (quad
     // walks: 6 waves/SIMD measured best, 423 vs 374 Msamples/s at 4 and 350 at 8)
@@ -1128,6 +1274,8 @@ static int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounce
     const int rows = src.xy ? 0 : n / src.W;
     while (nl > 1 && (n < nl * 65536 || (!src.xy && rows < nl))) nl--;
     WaveLane L[RT_MAX_LANES];
+    int force_fb = 0;
+    if (const char* e = getenv("RT_FORCE_FALLBACK")) force_fb = std::max(0, atoi(e));
     int tail_p = 5;  // (5 paths: 15 queries, one pass of the wave's 16 quads; sweep 2-6 within 1 %)
     if (const char* e = getenv("RT_TAIL_PATHS")) tail_p = std::min(RT_TAIL_MAXP, std::max(0, atoi(e)));
     const int tail_blocks = dev_cus * RT_TAIL_OCC;  // one grid-fill of k_tail
@@ -1186,6 +1334,7 @@ static int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounce
         W.budget = b->budget;
         W.counters = La.cnt;
         W.tail_paths = tail_p;
+        W.force_fb = force_fb;
         W.iterq = (S && iter_log && l == 0) ? (int32_t*)b->iterq.p : nullptr;
         La.lists[0] = (int32_t*)W.act_in;
         La.lists[1] = W.act_out;
@@ -1364,7 +1513,7 @@ static int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounce
     return RT_OK;
 }
 
-static int finish_stats(rt_context* c, Backend* b, hipStream_t s)
+int finish_stats(rt_context* c, Backend* b, hipStream_t s)
 {
     if (!c->stats_enabled) return RT_OK;
     HIPCHK(c, hipMemcpyAsync(c->stats, b->stats.p, sizeof(c->stats), hipMemcpyDeviceToHost, s));
@@ -1372,11 +1521,101 @@ static int finish_stats(rt_context* c, Backend* b, hipStream_t s)
     return RT_OK;
 }
 
+// Rows of a multi-device render: request row j (image row off + j*stride) belongs to
+// device j mod N. Device d's rows go to block d of the root's staging buffer (rows_max
+// rows each; the tail of a short block is padding), ncclScatter sends block d to
+// device d, every device renders its block with its own wavefront loop (one host
+// thread per device: run_wave polls its lanes), and ncclGather brings the blocks back
+// for the un-permute. Pack and un-permute are strided 2-D copies on the root.
+int render_multi(rt_context* c, Group* g, int w, int h, int spp, int bounces, float4_* fb, int off, int stride,
+                 hipStream_t s)
+{
+    const int N = (int)g->dev.size();
+    std::string err;
+    const Rccl* R = rccl_load(err);
+    if (!R) return rt_fail(c, RT_ERR_NODEV, err);
+    const int rows = (h - off + stride - 1) / stride;
+    const int rows_max = (rows + N - 1) / N;
+    const size_t blk = (size_t)rows_max * w;  // float4 per block
+    auto rows_of = [&](int d) { return rows > d ? (rows - d + N - 1) / N : 0; };
+    Backend* root = g->dev[0];
+    for (int d = 1; d < N; d++) {
+        HIPCHK(c, hipSetDevice(g->dev[d]->device));
+        if (int r = ensure(c, g->shard[d], std::max<size_t>(blk, 1) * sizeof(float4_))) return r;
+    }
+    HIPCHK(c, hipSetDevice(root->device));
+    if (int r = ensure(c, g->stage, std::max<size_t>(blk, 1) * N * sizeof(float4_))) return r;
+    float4_* stage = (float4_*)g->stage.p;
+    HIPCHK(c, hipEventRecord(root->ev0, s));
+    const size_t pitch = (size_t)w * sizeof(float4_);
+    for (int d = 0; d < N; d++)
+        if (rows_of(d))
+            HIPCHK(c, hipMemcpy2DAsync(stage + d * blk, pitch, fb + (size_t)d * w, N * pitch, pitch, rows_of(d),
+                                       hipMemcpyDeviceToDevice, s));
+    std::vector<hipStream_t> st(N);
+    for (int d = 0; d < N; d++) st[d] = d == 0 ? s : g->dev[d]->own;
+    const size_t cnt = blk * 4;  // floats per block
+    NCCLCHK(c, R, R->group_start());
+    for (int d = 0; d < N; d++)
+        NCCLCHK(c, R, R->scatter(stage, d == 0 ? (void*)stage : g->shard[d].p, cnt, ncclFloat, 0, g->comms[d], st[d]));
+    NCCLCHK(c, R, R->group_end());
+    // the wavefront loops, one host thread per device
+    std::vector<int> rc(N, RT_OK);
+    auto work = [&](int d) {
+        Backend* b = g->dev[d];
+        if (hipSetDevice(b->device) != hipSuccess) {
+            rc[d] = rt_fail(c, RT_ERR_HIP, "render: hipSetDevice failed");
+            return;
+        }
+        if (c->stats_enabled && hipMemsetAsync(b->stats.p, 0, b->stats.bytes, st[d]) != hipSuccess) {
+            rc[d] = rt_fail(c, RT_ERR_HIP, "render: stats reset failed");
+            return;
+        }
+        const rtk::PixSrc src{w, off + d * stride, N * stride, nullptr};
+        float4_* dst = d == 0 ? stage : (float4_*)g->shard[d].p;
+        rc[d] = run_wave(c, b, w, h, spp, bounces, src, rows_of(d) * w, dst, st[d]);
+    };
+    {
+        std::vector<std::thread> th;
+        for (int d = 1; d < N; d++) th.emplace_back(work, d);
+        work(0);
+        for (auto& t : th) t.join();
+    }
+    for (int d = 0; d < N; d++)
+        if (rc[d]) return rc[d];
+    HIPCHK(c, hipSetDevice(root->device));
+    NCCLCHK(c, R, R->group_start());
+    for (int d = 0; d < N; d++)
+        NCCLCHK(c, R, R->gather(d == 0 ? (const void*)stage : g->shard[d].p, stage, cnt, ncclFloat, 0, g->comms[d], st[d]));
+    NCCLCHK(c, R, R->group_end());
+    for (int d = 0; d < N; d++)
+        if (rows_of(d))
+            HIPCHK(c, hipMemcpy2DAsync(fb + (size_t)d * w, N * pitch, stage + d * blk, pitch, pitch, rows_of(d),
+                                       hipMemcpyDeviceToDevice, s));
+    HIPCHK(c, hipEventRecord(root->ev1, s));
+    if (c->stats_enabled) {  // counters summed over the devices
+        unsigned long long sum[2 * RT_STAT_COUNT] = {};
+        for (int d = 0; d < N; d++) {
+            HIPCHK(c, hipSetDevice(g->dev[d]->device));
+            HIPCHK(c, hipMemcpyAsync(c->stats, g->dev[d]->stats.p, sizeof(c->stats), hipMemcpyDeviceToHost, st[d]));
+            HIPCHK(c, hipStreamSynchronize(st[d]));
+            for (int i = 0; i < 2 * RT_STAT_COUNT; i++) sum[i] += c->stats[i];
+        }
+        std::memcpy(c->stats, sum, sizeof sum);
+        HIPCHK(c, hipSetDevice(root->device));
+    }
+    root->last_iters = 0;
+    for (Backend* b : g->dev) root->last_iters = std::max(root->last_iters, b->last_iters);
+    return RT_OK;
+}
+}  // namespace
+
 int rt_backend_render(rt_context* c, int w, int h, int spp, int bounces, float* host_fb, void* dev_fb, int row_offset,
                       int row_stride, void* stream)
 {
+    Group* g = grp(c);
     Backend* b = be(c);
-    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipSetDevice(b->device));
     hipStream_t s = (hipStream_t)stream;
     const int rows_local = (h - row_offset + row_stride - 1) / row_stride;
     const size_t npx = (size_t)rows_local * w;
@@ -1387,10 +1626,14 @@ int rt_backend_render(rt_context* c, int w, int h, int spp, int bounces, float* 
         fb = (float4_*)b->fb.p;
         HIPCHK(c, hipMemcpyAsync(fb, host_fb, npx * sizeof(float4_), hipMemcpyHostToDevice, s));
     }
-    rtk::PixSrc src{w, row_offset, row_stride, nullptr};
-    HIPCHK(c, hipEventRecord(b->ev0, s));
-    if (int r = run_wave(c, b, w, h, spp, bounces, src, (int)npx, fb, s)) return r;
-    HIPCHK(c, hipEventRecord(b->ev1, s));
+    if (g->multi) {
+        if (int r = render_multi(c, g, w, h, spp, bounces, fb, row_offset, row_stride, s)) return r;
+    } else {
+        rtk::PixSrc src{w, row_offset, row_stride, nullptr};
+        HIPCHK(c, hipEventRecord(b->ev0, s));
+        if (int r = run_wave(c, b, w, h, spp, bounces, src, (int)npx, fb, s)) return r;
+        HIPCHK(c, hipEventRecord(b->ev1, s));
+    }
     if (host_fb) {
         HIPCHK(c, hipMemcpyAsync(host_fb, fb, npx * sizeof(float4_), hipMemcpyDeviceToHost, s));
         HIPCHK(c, hipStreamSynchronize(s));
@@ -1400,33 +1643,82 @@ int rt_backend_render(rt_context* c, int w, int h, int spp, int bounces, float* 
     } else {
         c->last_kernel_ms = -1.0;  // read with rt_device_last_kernel_ms after the caller synchronizes
     }
-    return finish_stats(c, b, s);
+    return g->multi ? RT_OK : finish_stats(c, b, s);
+}
+
+// One device's share of a pixel list (host buffers in and out).
+static int render_pixels_one(rt_context* c, Backend* b, int w, int h, int spp, int bounces, const int* xy, int n,
+                             float* rgba, float* ms_out)
+{
+    HIPCHK(c, hipSetDevice(b->device));
+    if (n == 0) return RT_OK;
+    const size_t bxy = (size_t)n * 8, brgba = (size_t)n * 16;
+    if (int r = ensure(c, b->xy, bxy)) return r;
+    if (int r = ensure(c, b->fb, brgba)) return r;
+    hipStream_t s = b->own;
+    HIPCHK(c, hipMemcpyAsync(b->xy.p, xy, bxy, hipMemcpyHostToDevice, s));
+    HIPCHK(c, hipMemcpyAsync(b->fb.p, rgba, brgba, hipMemcpyHostToDevice, s));
+    if (c->stats_enabled) HIPCHK(c, hipMemsetAsync(b->stats.p, 0, b->stats.bytes, s));
+    rtk::PixSrc src{w, 0, 1, (const int32_t*)b->xy.p};
+    HIPCHK(c, hipEventRecord(b->ev0, s));
+    if (int r = run_wave(c, b, w, h, spp, bounces, src, n, (float4_*)b->fb.p, s)) return r;
+    HIPCHK(c, hipEventRecord(b->ev1, s));
+    HIPCHK(c, hipMemcpyAsync(rgba, b->fb.p, brgba, hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipStreamSynchronize(s));
+    float ms = 0;
+    HIPCHK(c, hipEventElapsedTime(&ms, b->ev0, b->ev1));
+    *ms_out = ms;
+    return RT_OK;
 }
 
 int rt_backend_render_pixels(rt_context* c, int w, int h, int spp, int bounces, const int* xy, int n, float* rgba)
 {
-    Backend* b = be(c);
-    HIPCHK(c, hipSetDevice(c->device));
-    const size_t bxy = (size_t)n * 8, brgba = (size_t)n * 16;
-    if (int r = ensure(c, b->xy, bxy)) return r;
-    if (int r = ensure(c, b->fb, brgba)) return r;
-    HIPCHK(c, hipMemcpy(b->xy.p, xy, bxy, hipMemcpyHostToDevice));
-    HIPCHK(c, hipMemcpy(b->fb.p, rgba, brgba, hipMemcpyHostToDevice));
-    rtk::PixSrc src{w, 0, 1, (const int32_t*)b->xy.p};
-    HIPCHK(c, hipEventRecord(b->ev0, 0));
-    if (int r = run_wave(c, b, w, h, spp, bounces, src, n, (float4_*)b->fb.p, 0)) return r;
-    HIPCHK(c, hipEventRecord(b->ev1, 0));
-    HIPCHK(c, hipMemcpy(rgba, b->fb.p, brgba, hipMemcpyDeviceToHost));
-    float ms = 0;
-    HIPCHK(c, hipEventElapsedTime(&ms, b->ev0, b->ev1));
-    c->last_kernel_ms = ms;
-    return finish_stats(c, b, 0);
+    Group* g = grp(c);
+    const int N = (int)g->dev.size();
+    if (N == 1) {
+        float ms = 0;
+        if (int r = render_pixels_one(c, g->dev[0], w, h, spp, bounces, xy, n, rgba, &ms)) return r;
+        c->last_kernel_ms = ms;
+        return finish_stats(c, g->dev[0], g->dev[0]->own);
+    }
+    // pixel i -> device i mod N (pixels are independent); host-side split and merge
+    std::vector<std::vector<int>> pxy(N);
+    std::vector<std::vector<float>> prgba(N);
+    for (int i = 0; i < n; i++) {
+        pxy[i % N].push_back(xy[2 * i]);
+        pxy[i % N].push_back(xy[2 * i + 1]);
+        prgba[i % N].insert(prgba[i % N].end(), rgba + 4 * (size_t)i, rgba + 4 * (size_t)i + 4);
+    }
+    std::vector<int> rc(N, RT_OK);
+    std::vector<float> ms(N, 0.0f);
+    {
+        std::vector<std::thread> th;
+        for (int d = 0; d < N; d++)
+            th.emplace_back([&, d] {
+                rc[d] = render_pixels_one(c, g->dev[d], w, h, spp, bounces, pxy[d].data(), (int)pxy[d].size() / 2,
+                                          prgba[d].data(), &ms[d]);
+            });
+        for (auto& t : th) t.join();
+    }
+    for (int d = 0; d < N; d++)
+        if (rc[d]) return rc[d];
+    for (int i = 0; i < n; i++) std::memcpy(rgba + 4 * (size_t)i, &prgba[i % N][4 * (size_t)(i / N)], 16);
+    c->last_kernel_ms = *std::max_element(ms.begin(), ms.end());
+    if (c->stats_enabled) {
+        unsigned long long sum[2 * RT_STAT_COUNT] = {};
+        for (int d = 0; d < N; d++) {
+            if (int r = finish_stats(c, g->dev[d], g->dev[d]->own)) return r;
+            for (int i = 0; i < 2 * RT_STAT_COUNT; i++) sum[i] += c->stats[i];
+        }
+        std::memcpy(c->stats, sum, sizeof sum);
+    }
+    return RT_OK;
 }
 
 int rt_backend_intersect(rt_context* c, const float* rays, int n, void* out)
 {
     Backend* b = be(c);
-    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipSetDevice(b->device));
     const size_t br = (size_t)n * 24, bo = (size_t)n * 44;
     if (int r = ensure(c, b->xy, br + bo)) return r;
     float* dr = (float*)b->xy.p;
@@ -1471,13 +1763,13 @@ extern "C" int rt_device_queries(rt_context* c, int mode, const float* rays, int
 {
     if (!c || !c->backend || n <= 0 || reps < 1) return RT_ERR_ARG;
     Backend* b = be(c);
-    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipSetDevice(b->device));
     if (c->dirty) {
         if (int r = rt_backend_upload(c)) return r;
         c->dirty = false;
     }
     int cus = 256;
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, b->device);
     const int threads = 256, blocks = std::min((n + threads - 1) / threads, cus * 8);
     const int qblocks = std::min((4 * n + threads - 1) / threads, cus * 16);
     float4_* d_rays = nullptr;
@@ -1539,19 +1831,33 @@ extern "C" double rt_device_last_kernel_ms(rt_context* c)
 // Iterations the last wavefront render took.
 extern "C" int rt_device_last_iterations(rt_context* c) { return c && c->backend ? be(c)->last_iters : -1; }
 
-// Per-kernel-class timing (k_trace, k_step, reserved) over
-// the renders since it was enabled: out_ms[3] total ms, out_launches[3].
+// Per-kernel-class timing (k_trace, k_step, k_tail) over the renders since it
+// was enabled, summed over the context's devices: out_ms[3] total ms (HIP events
+// around every launch on its lane's stream), out_launches[3].
 extern "C" int rt_device_kernel_timing(rt_context* c, int enable, double* out_ms, long* out_launches)
 {
     if (!c || !c->backend) return RT_ERR_ARG;
-    Backend* b = be(c);
-    if (out_ms)
-        for (int k = 0; k < 3; k++) out_ms[k] = b->kms[k];
-    if (out_launches)
-        for (int k = 0; k < 3; k++) out_launches[k] = b->klaunch[k];
-    if (enable >= 0) {
-        b->timing = enable != 0;
-        for (int k = 0; k < 3; k++) b->kms[k] = 0, b->klaunch[k] = 0;
+    Group* g = grp(c);
+    for (int k = 0; k < 3; k++) {
+        double ms = 0;
+        long n = 0;
+        for (Backend* b : g->dev) ms += b->kms[k], n += b->klaunch[k];
+        if (out_ms) out_ms[k] = ms;
+        if (out_launches) out_launches[k] = n;
     }
+    if (enable >= 0)
+        for (Backend* b : g->dev) {
+            b->timing = enable != 0;
+            for (int k = 0; k < 3; k++) b->kms[k] = 0, b->klaunch[k] = 0;
+        }
+    return RT_OK;
+}
+
+// Wavefront lanes (streams) per render on every device of the context (RT_LANES at
+// creation; 1 serializes a render's launches, for per-launch kernel timing).
+extern "C" int rt_device_set_lanes(rt_context* c, int lanes)
+{
+    if (!c || !c->backend || lanes < 1) return RT_ERR_ARG;
+    for (Backend* b : grp(c)->dev) b->lanes = std::min(RT_MAX_LANES, lanes);
     return RT_OK;
 }

@@ -119,6 +119,8 @@ struct WaveView {
     int32_t* iterq;         // stats renders: [iteration][2] = {queries, live slots} (else null)
     int iter;               // iteration of this launch
     int tail_paths;         // k_tail: paths per wave
+    int force_fb;           // test knob (RT_FORCE_FALLBACK): a query whose ray hashes to 0 mod force_fb
+                            // skips the quad walk and takes the exact octree walk (0: off)
     int shards, seg_cap;    // queues and live lists: `shards` segments of seg_cap entries (device: rt_render.hip)
     const int32_t* act_in;  // active slots this iteration
     int32_t* act_out;

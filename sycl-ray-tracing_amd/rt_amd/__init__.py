@@ -185,20 +185,34 @@ class BVH:
 class RenderKernel:
     """RenderKernel(width, height, render_samples, max_bounces, image_buffer,
     triangles, materials, emissive_triangle_indices, materials_indices,
-    analytic_spheres, bvh, skysphere, env_map_cdf) — render_kernel.h:24-46."""
+    analytic_spheres, bvh, skysphere, env_map_cdf) — render_kernel.h:24-46.
+
+    device: a HIP ordinal, or a sequence of them for one context over several
+    GPUs (rt_create_multi: rows sharded over the devices, RCCL scatter/gather
+    through the first). Like the reference, which keeps a reference to the
+    material vector (render_kernel.h:81-93), a render picks up in-place edits
+    of `materials_buffer` (rt_set_materials: no BVH rebuild); the triangles,
+    BVH and sky are bound at construction."""
 
     def __init__(self, width, height, render_samples, max_bounces, image_buffer: Image, triangle_buffer,
                  materials_buffer, emissive_triangle_indices_buffer, materials_indices_buffer, analytic_spheres_buffer,
-                 bvh: BVH, skysphere: Image, env_map_cdf, device: int = 0, hostsim: bool = False):
+                 bvh: BVH, skysphere: Image, env_map_cdf, device=0, hostsim: bool = False):
         self.L = lib(hostsim)
         self.width, self.height = int(width), int(height)
         self.render_samples, self.max_bounces = int(render_samples), int(max_bounces)
         self.frame_buffer = image_buffer
         h = ctypes.c_void_p()
-        check(self.L, self.L.rt_create(device, ctypes.byref(h)), None, "rt_create")
+        if isinstance(device, (list, tuple)):
+            ids = np.ascontiguousarray(device, dtype=np.int32)
+            check(self.L, self.L.rt_create_multi(ids.shape[0], ptr(ids), ctypes.byref(h)), None, "rt_create_multi")
+        else:
+            check(self.L, self.L.rt_create(int(device), ctypes.byref(h)), None, "rt_create")
         self.ctx = h
+        self.n_devices = int(self.L.rt_device_count(self.ctx))
         tris = np.ascontiguousarray(triangle_buffer, dtype=np.float32).reshape(-1, 9)
         mats = np.ascontiguousarray(materials_buffer, dtype=np.float32).reshape(-1, 10)
+        self.materials_buffer = materials_buffer if isinstance(materials_buffer, np.ndarray) else mats
+        self._mats_sent = mats.copy()
         em = np.ascontiguousarray(emissive_triangle_indices_buffer, dtype=np.int32)
         mi = np.ascontiguousarray(materials_indices_buffer, dtype=np.int32)
         sph = np.ascontiguousarray(analytic_spheres_buffer if analytic_spheres_buffer is not None else np.zeros((0, 5)),
@@ -227,7 +241,20 @@ class RenderKernel:
         check(self.L, self.L.rt_set_camera(self.ctx, ptr(camera.view_matrix), camera.fov_dist), self.ctx,
               "rt_set_camera")
 
+    def _sync_materials(self):
+        """Push the material table again if the caller edited it in place."""
+        m = np.ascontiguousarray(self.materials_buffer, dtype=np.float32).reshape(-1, 10)
+        if m.shape != self._mats_sent.shape or not np.array_equal(m.view(np.uint32), self._mats_sent.view(np.uint32)):
+            self.set_materials(m)
+
+    def set_materials(self, materials):
+        """rt_set_materials: a new material table for the bound scene (the cfg5 sweep)."""
+        m = np.ascontiguousarray(materials, dtype=np.float32).reshape(-1, 10)
+        check(self.L, self.L.rt_set_materials(self.ctx, ptr(m), m.shape[0]), self.ctx, "rt_set_materials")
+        self._mats_sent = m.copy()
+
     def render(self):
+        self._sync_materials()
         fb = self.frame_buffer.pixels
         assert fb.flags.c_contiguous and fb.dtype == np.float32 and fb.shape == (self.height, self.width, 4)
         check(self.L, self.L.rt_render(self.ctx, self.width, self.height, self.render_samples, self.max_bounces,
@@ -235,12 +262,14 @@ class RenderKernel:
 
     def render_device(self, d_fb: int, row_offset: int = 0, row_stride: int = 1, stream: int | None = None):
         """Render into a device buffer (e.g. a torch tensor's data_ptr()); no host copies."""
+        self._sync_materials()
         check(self.L, self.L.rt_render_device(self.ctx, self.width, self.height, self.render_samples,
                                               self.max_bounces, ctypes.c_void_p(d_fb), row_offset, row_stride,
                                               ctypes.c_void_p(stream) if stream else None), self.ctx,
               "rt_render_device")
 
     def ray_trace_pixels(self, xy) -> None:
+        self._sync_materials()
         xy = np.ascontiguousarray(xy, dtype=np.int32).reshape(-1, 2)
         fb = self.frame_buffer.pixels
         rgba = np.ascontiguousarray(fb[xy[:, 1], xy[:, 0]])
@@ -279,13 +308,18 @@ class RenderKernel:
     def kernel_timing(self, enable: int = -1):
         """Per-kernel-class GPU time (HIP events around every launch) since
         timing was last enabled: {class: (total_ms, launches)} for the
-        query kernel (k_trace, with its exact-walk role) and the path step
-        (k_step); "other" is reserved. enable=1/0
+        query kernel (k_trace), the path step (k_step, with the exact-walk
+        roles) and "other" (the tail kernel k_tail), summed over the
+        context's devices. enable=1/0
         turns timing on/off and resets the totals; -1 only reads."""
         ms = np.zeros(3, dtype=np.float64)
         n = np.zeros(3, dtype=np.int64)
         check(self.L, self.L.rt_device_kernel_timing(self.ctx, enable, ptr(ms), ptr(n)), self.ctx, "kernel_timing")
         return {k: (float(a), int(b)) for k, a, b in zip(("trace", "step", "other"), ms, n)}
+
+    def set_lanes(self, lanes: int):
+        """Wavefront lanes (streams) per render on every device (1: launches serialized)."""
+        check(self.L, self.L.rt_device_set_lanes(self.ctx, int(lanes)), self.ctx, "rt_device_set_lanes")
 
     def last_iterations(self) -> int:
         return int(self.L.rt_device_last_iterations(self.ctx))

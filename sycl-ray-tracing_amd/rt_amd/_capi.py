@@ -23,7 +23,7 @@ EXPORTS = [
     "rt_render_device", "rt_render_pixels", "rt_intersect", "rt_set_stats", "rt_get_stats", "rt_last_kernel_ms",
     "rt_mesh_load", "rt_mesh_counts", "rt_mesh_copy", "rt_mesh_free", "rt_camera_preset", "rt_env_luminance_cdf",
     "rt_octree_dump", "rt_read_hdr", "rt_write_png", "rt_image_to_rgba8",
-    "rt_set_intersect_mode",
+    "rt_set_intersect_mode", "rt_create_multi", "rt_device_count", "rt_set_materials",
 ]
 
 P = ctypes.c_void_p
@@ -33,6 +33,9 @@ F = ctypes.c_float
 
 _SIGS = {
     "rt_create": (I, [I, ctypes.POINTER(P)]),
+    "rt_create_multi": (I, [I, P, ctypes.POINTER(P)]),
+    "rt_device_count": (I, [P]),
+    "rt_set_materials": (I, [P, P, I]),
     "rt_destroy": (None, [P]),
     "rt_last_error": (ctypes.c_char_p, [P]),
     "rt_version": (I, []),
@@ -65,6 +68,7 @@ _SIGS = {
     "rt_device_libm": (I, [I, I, P, P, P, I]),
     "rt_device_last_kernel_ms": (ctypes.c_double, [P]),
     "rt_device_kernel_timing": (I, [P, I, P, P]),
+    "rt_device_set_lanes": (I, [P, I]),
     "rt_device_last_iterations": (I, [P]),
     "rt_device_queries": (I, [P, I, P, I, I, P, P, P]),
     # hostsim-only extra

@@ -39,16 +39,17 @@ def golden_case(name: str, manifest: dict) -> dict:
 
 
 def make_kernel(entry: dict, cameras: dict, hostsim: bool, W=None, H=None, spp=None, bounces=None, fb=None,
-                spheres=None):
+                spheres=None, device=0, materials=None):
     P = parsed_scene(entry["scene"])
     W = W or entry["W"]
     H = H or entry["H"]
     fb = fb if fb is not None else rt_amd.Image(W, H)
     c = cameras[entry["camera"]]
     rk = rt_amd.RenderKernel(W, H, spp or entry["spp"], bounces or entry["bounces"], fb, P.triangles,
-                             materials_for(entry, P), P.emissive_triangle_indices, P.material_indices, spheres,
+                             materials if materials is not None else materials_for(entry, P),
+                             P.emissive_triangle_indices, P.material_indices, spheres,
                              rt_amd.BVH(P.triangles), rt_amd.Image.from_rgb(sky(entry["sky"])), None,
-                             hostsim=hostsim)
+                             hostsim=hostsim, device=device)
     rk.set_camera(rt_amd.Camera(c[:16], c[16]))
     return rk, fb
 

@@ -281,15 +281,19 @@ def test_gpu_tiny_scenes_match_oracle(n, cameras):
     assert_parity(got, want, min_bitwise=1.0)
 
 
+@pytest.mark.parametrize("tail", ["0", "5"])
 @pytest.mark.parametrize("name", ["mis_512", "cfg2_dragon", "cornell32_128"])
-def test_gpu_parked_walks_small_launches(name, manifest, cameras, monkeypatch):
-    """Exact-walk hand-off under stress: a step budget of 1 parks
-    every exact walk at its first node boundary, and with the tail kernel off
-    the last iterations run k_step on a live count of a few paths, where the
-    grid is smallest while fallbacks and parked walks are still pending. Every
-    pixel must still be written, bit for bit the reference's."""
+def test_gpu_parked_walks_small_launches(name, tail, manifest, cameras, monkeypatch):
+    """Exact-walk hand-off under stress: every 7th query (by a hash
+    of its ray, RT_FORCE_FALLBACK) skips the quad walk for the exact octree
+    walk, a step budget of 1 parks each of those walks at its first node
+    boundary, and with the tail kernel off the last iterations run k_step on a
+    live count of a few paths while fallbacks and parked walks are pending
+    (with it on, k_tail walks them inline). Every pixel must still be written,
+    bit for bit the reference's."""
     monkeypatch.setenv("RT_STEP_BUDGET", "1")
-    monkeypatch.setenv("RT_TAIL_PATHS", "0")
+    monkeypatch.setenv("RT_TAIL_PATHS", tail)
+    monkeypatch.setenv("RT_FORCE_FALLBACK", "7")
     e = rt_cases.golden_case(name, manifest)
     rk, fb = rt_cases.make_kernel(e, cameras, hostsim=False)
     rk.set_stats(True)
@@ -300,5 +304,6 @@ def test_gpu_parked_walks_small_launches(name, manifest, cameras, monkeypatch):
         rk.ray_trace_pixels(e["px"])
         got = fb.pixels[e["px"][:, 1], e["px"][:, 0]]
     st = rk.stats()
-    print(name, "fallbacks", st["fallback"], "iterations", rk.last_iterations())
+    print(name, "fallbacks", st["fallback"], "in k_tail", st["tail_fallback"], "iterations", rk.last_iterations())
+    assert st["fallback"] > 0
     assert_parity(got, e["expected"], min_bitwise=1.0)
