@@ -1460,7 +1460,9 @@ int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounces, cons
             if (!La.done) {
                 if (La.it >= max_iters) {
                     HIPCHK(c, hipStreamSynchronize(La.s));
-                    return rt_fail(c, RT_ERR_STATE, "render: wavefront loop did not drain");
+                    return rt_fail(c, RT_ERR_STATE, "render: wavefront loop did not drain in " +
+                                                            std::to_string(max_iters) + " iterations (step budget " +
+                                                            std::to_string(b->budget) + ")");
                 }
                 if (int r = issue(La)) return r;
                 any = true;

@@ -282,18 +282,19 @@ def test_gpu_tiny_scenes_match_oracle(n, cameras):
 
 
 @pytest.mark.parametrize("tail", ["0", "5"])
-@pytest.mark.parametrize("name", ["mis_512", "cfg2_dragon", "cornell32_128"])
-def test_gpu_parked_walks_small_launches(name, tail, manifest, cameras, monkeypatch):
-    """Exact-walk hand-off under stress: every 7th query (by a hash
-    of its ray, RT_FORCE_FALLBACK) skips the quad walk for the exact octree
-    walk, a step budget of 1 parks each of those walks at its first node
-    boundary, and with the tail kernel off the last iterations run k_step on a
-    live count of a few paths while fallbacks and parked walks are pending
+@pytest.mark.parametrize("name,budget,every", [("mis_512", 1, 7), ("cornell32_128", 1, 7), ("cfg2_dragon", 8, 31)])
+def test_gpu_parked_walks_small_launches(name, budget, every, tail, manifest, cameras, monkeypatch):
+    """Exact-walk hand-off under stress: every `every`-th query (by
+    a hash of its ray, RT_FORCE_FALLBACK) skips the quad walk for the exact
+    octree walk, a step budget of 1 (8 on the dragon, whose walks take ~200
+    steps: each park costs an iteration) parks those walks at node
+    boundaries, and with the tail kernel off the last iterations run k_step on
+    a live count of a few paths while fallbacks and parked walks are pending
     (with it on, k_tail walks them inline). Every pixel must still be written,
     bit for bit the reference's."""
-    monkeypatch.setenv("RT_STEP_BUDGET", "1")
+    monkeypatch.setenv("RT_STEP_BUDGET", str(budget))
     monkeypatch.setenv("RT_TAIL_PATHS", tail)
-    monkeypatch.setenv("RT_FORCE_FALLBACK", "7")
+    monkeypatch.setenv("RT_FORCE_FALLBACK", str(every))
     e = rt_cases.golden_case(name, manifest)
     rk, fb = rt_cases.make_kernel(e, cameras, hostsim=False)
     rk.set_stats(True)
