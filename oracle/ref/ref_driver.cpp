@@ -7,13 +7,12 @@
 // It exists to produce golden fixtures (tests/golden/) and the
 // "reference"-kind CPU timing. Nothing in the product links it.
 //
-// Two pieces of the reference cannot be compiled here without stand-ins
-// (source/utils.cpp pulls in Intel OIDN, whose libraries are absent), so the
-// driver restates them on top of the vendored rapidobj / the reference types:
-//   parse_obj           <- source/utils.cpp:16-98
-//   compute_env_map_cdf <- source/utils.cpp:126-142
-//   read_image_float    <- source/utils.cpp:100-124 (HDR decode replaced by a
-//                          raw RGB f32 file; the env map asset is absent)
+// Scene ingest is the reference's own source/utils.cpp (Utils::parse_obj,
+// Utils::compute_env_map_cdf), compiled and linked by the Makefile. Only the
+// env image loader is replaced: the HDR asset is absent, so the synthetic sky
+// comes in as a raw RGB f32 file (read_env_raw) and is stored as the same
+// Image the reference's read_image_float builds (Color(r, g, b, 0),
+// utils.cpp:114-120).
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -35,63 +34,22 @@
 #include "simple_material.h"
 #include "sphere.h"
 #include "triangle.h"
+#include "utils.h"
 
-// ---------------------------------------------------------------- restated
-static ParsedOBJ parse_obj(const std::string& filepath)  // utils.cpp:16-98
-{
-    ParsedOBJ parsed_obj;
-    rapidobj::Result res = rapidobj::ParseFile(filepath, rapidobj::MaterialLibrary::Default());
-    if (res.error) {
-        std::fprintf(stderr, "OBJ error: %s\n", res.error.code.message().c_str());
-        std::exit(1);
-    }
-    rapidobj::Triangulate(res);
-    const rapidobj::Array<float>& positions = res.attributes.positions;
-    for (rapidobj::Shape& shape : res.shapes) {
-        rapidobj::Mesh& mesh = shape.mesh;
-        for (size_t i = 0; i < mesh.indices.size(); i += 3) {
-            int i0 = mesh.indices[i + 0].position_index;
-            int i1 = mesh.indices[i + 1].position_index;
-            int i2 = mesh.indices[i + 2].position_index;
-            Point A(positions[i0 * 3 + 0], positions[i0 * 3 + 1], positions[i0 * 3 + 2]);
-            Point B(positions[i1 * 3 + 0], positions[i1 * 3 + 1], positions[i1 * 3 + 2]);
-            Point C(positions[i2 * 3 + 0], positions[i2 * 3 + 1], positions[i2 * 3 + 2]);
-            parsed_obj.triangles.push_back(Triangle(A, B, C));
-            int mat = mesh.material_ids[i / 3];
-            parsed_obj.material_indices.push_back(mat + 1);
-            rapidobj::Float3 emission;
-            if (mat == -1)
-                emission = rapidobj::Float3{0, 0, 0};
-            else
-                emission = res.materials[mat].emission;
-            if (emission[0] > 0 || emission[1] > 0 || emission[2] > 0)
-                parsed_obj.emissive_triangle_indices.push_back((int)parsed_obj.triangles.size() - 1);
-        }
-    }
-    parsed_obj.materials.push_back(SimpleMaterial{Color(1.0f, 0.0f, 1.0f), Color(), 0.0f, 1.0f});
-    for (const rapidobj::Material& m : res.materials) {
-        SimpleMaterial sm = SimpleMaterial{Color(m.emission), Color(m.diffuse), m.metallic, m.roughness};
-        sm.roughness = std::max(1.0e-2f, sm.roughness);
-        if (m.illum == 0) {
-            SimpleMaterial def;
-            sm.roughness = def.roughness;
-            sm.metalness = def.metalness;
-        }
-        parsed_obj.materials.push_back(sm);
-    }
-    return parsed_obj;
-}
+// ---------------------------------------------------------------- inputs
+static ParsedOBJ parse_obj(const std::string& filepath) { return Utils::parse_obj(filepath); }
+static std::vector<float> compute_env_map_cdf(const Image& sky) { return Utils::compute_env_map_cdf(sky); }
 
-static std::vector<float> compute_env_map_cdf(const Image& sky)  // utils.cpp:126-142
+// main.cpp:20-30 add_sphere_to_scene (main.cpp holds main(), so it is not linked):
+// the sphere's material is appended to the materials and its material index to
+// material_indices; the sphere's primitive index is the caller's.
+static Sphere add_sphere_to_scene(ParsedOBJ& parsed_obj, const Point& center, float radius,
+                                  const SimpleMaterial& material, int primitive_index)
 {
-    std::vector<float> out(sky.height() * sky.width());
-    out[0] = 0.0f;
-    for (int y = 0; y < sky.height(); y++)
-        for (int x = 0; x < sky.width(); x++) {
-            int index = y * sky.width() + x;
-            out[index] = out[std::max(index - 1, 0)] + sky.luminance_of_pixel(x, y);
-        }
-    return out;
+    int material_index = parsed_obj.materials.size();
+    parsed_obj.materials.push_back(material);
+    parsed_obj.material_indices.push_back(material_index);
+    return Sphere(center, radius, primitive_index);
 }
 
 static Image read_env_raw(const char* path)  // raw stand-in for utils.cpp:100-124
@@ -163,10 +121,36 @@ struct Scene {
     std::vector<float> cdf;
 };
 
+// RT_SPHERES="cx,cy,cz,r,er,eg,eb,dr,dg,db,metalness,roughness;..." adds analytic
+// spheres the way main.cpp:74 would with add_sphere_to_scene (primitive index of
+// sphere k: the triangle count + k, as main.cpp:74 passes triangles.size()).
+static void add_env_spheres(Scene& s)
+{
+    const char* e = std::getenv("RT_SPHERES");
+    if (!e) return;
+    std::string spec(e);
+    size_t pos = 0;
+    while (pos < spec.size()) {
+        size_t end = spec.find(';', pos);
+        if (end == std::string::npos) end = spec.size();
+        float v[12];
+        if (std::sscanf(spec.substr(pos, end - pos).c_str(), "%f,%f,%f,%f,%f,%f,%f,%f,%f,%f,%f,%f", &v[0], &v[1], &v[2],
+                        &v[3], &v[4], &v[5], &v[6], &v[7], &v[8], &v[9], &v[10], &v[11]) != 12) {
+            std::fprintf(stderr, "bad RT_SPHERES entry\n");
+            std::exit(2);
+        }
+        SimpleMaterial m{Color(v[4], v[5], v[6]), Color(v[7], v[8], v[9]), v[10], v[11]};
+        const int prim = (int)s.obj.triangles.size() + (int)s.spheres.size();
+        s.spheres.push_back(add_sphere_to_scene(s.obj, Point(v[0], v[1], v[2]), v[3], m, prim));
+        pos = end + 1;
+    }
+}
+
 static void load_scene(Scene& s, const char* obj, const char* env)
 {
     s.obj = parse_obj(obj);
     s.bvh = new BVH(&s.obj.triangles);
+    add_env_spheres(s);
     if (env) {
         s.sky = read_env_raw(env);
         s.cdf = compute_env_map_cdf(s.sky);

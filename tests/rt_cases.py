@@ -29,6 +29,33 @@ def materials_for(entry: dict, P) -> np.ndarray:
     return mats
 
 
+def sphere_buffers(entry: dict, P, mats: np.ndarray):
+    """(materials, material_indices, spheres) with the entry's analytic spheres
+    added the way main.cpp:20-30 add_sphere_to_scene does: each sphere's
+    material appended to the materials, its material index to the material
+    indices, primitive index = triangle count + k (gen_golden.py, ref_driver)."""
+    sph = entry.get("spheres")
+    if not sph:
+        return mats, P.material_indices, None
+    sph = np.asarray(sph, np.float32).reshape(-1, 12)
+    n_tris = P.triangles.shape[0]
+    new_mats = [mats]
+    mi = [P.material_indices]
+    spheres = np.zeros((sph.shape[0], 5), np.float32)
+    for k, row in enumerate(sph):
+        m = np.zeros((1, 10), np.float32)
+        m[0, 0:3] = row[4:7]          # emission (alpha 1: Color(r, g, b))
+        m[0, 3] = 1.0
+        m[0, 4:7] = row[7:10]         # diffuse
+        m[0, 7] = 1.0
+        m[0, 8], m[0, 9] = row[10], row[11]
+        mi.append(np.array([mats.shape[0] + k], np.int32))
+        new_mats.append(m)
+        spheres[k, :4] = row[:4]
+        spheres[k, 4] = n_tris + k
+    return np.concatenate(new_mats), np.concatenate(mi).astype(np.int32), spheres
+
+
 def golden_case(name: str, manifest: dict) -> dict:
     e = dict(manifest["renders"][name])
     g = load_golden(f"render_{name}.npz")
@@ -45,9 +72,12 @@ def make_kernel(entry: dict, cameras: dict, hostsim: bool, W=None, H=None, spp=N
     H = H or entry["H"]
     fb = fb if fb is not None else rt_amd.Image(W, H)
     c = cameras[entry["camera"]]
+    mats = materials if materials is not None else materials_for(entry, P)
+    mi = P.material_indices
+    if spheres is None and entry.get("spheres"):
+        mats, mi, spheres = sphere_buffers(entry, P, mats)
     rk = rt_amd.RenderKernel(W, H, spp or entry["spp"], bounces or entry["bounces"], fb, P.triangles,
-                             materials if materials is not None else materials_for(entry, P),
-                             P.emissive_triangle_indices, P.material_indices, spheres,
+                             mats, P.emissive_triangle_indices, mi, spheres,
                              rt_amd.BVH(P.triangles), rt_amd.Image.from_rgb(sky(entry["sky"])), None,
                              hostsim=hostsim, device=device)
     rk.set_camera(rt_amd.Camera(c[:16], c[16]))
@@ -68,8 +98,8 @@ def run_case(entry: dict, cameras: dict, hostsim: bool) -> np.ndarray:
 def oracle_scene(entry: dict):
     from oracle_bindings import OracleScene
     P = parsed_scene(entry["scene"])
-    return OracleScene(P.triangles, P.material_indices, materials_for(entry, P), P.emissive_triangle_indices,
-                       env=sky(entry["sky"]))
+    mats, mi, spheres = sphere_buffers(entry, P, materials_for(entry, P))
+    return OracleScene(P.triangles, mi, mats, P.emissive_triangle_indices, env=sky(entry["sky"]), spheres=spheres)
 
 
 def run_oracle(entry: dict, cameras: dict, threads: int = 0) -> np.ndarray:
@@ -79,8 +109,10 @@ def run_oracle(entry: dict, cameras: dict, threads: int = 0) -> np.ndarray:
     return res
 
 
-CORNELL_CASES = ["cfg1_cornell12", "cornell32_128", "cornell32_64spp", "mis_512"]
-DRAGON_CASES = ["cfg2_dragon", "cfg3_dragon", "cfg4_dragon4k"] + [
+CORNELL_CASES = ["cfg1_cornell12", "cornell32_128", "cornell32_64spp", "mis_512", "spheres_cornell32_128",
+                 "spheres_cornell32_64spp"]
+SPHERE_CASES = ["spheres_cornell32_128", "spheres_cornell32_64spp", "spheres_dragon"]
+DRAGON_CASES = ["cfg2_dragon", "cfg3_dragon", "cfg4_dragon4k", "spheres_dragon"] + [
     f"cfg5_sweep_m{m}_r{r}" for m in range(4) for r in range(4)]
 
 

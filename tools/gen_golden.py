@@ -25,7 +25,15 @@ import scenes  # noqa: E402
 REF = os.path.join(gio.REPO, "oracle", "_ref", "ref_driverO2")
 OUT = gio.GOLDEN
 
-# (name, scene, sky, camera, W, H, spp, bounces, pixels or None for full frame, mat override)
+# analytic spheres (main.cpp:20-30 add_sphere_to_scene): 12 floats each,
+# center xyz, radius, emission rgb, diffuse rgb, metalness, roughness. Non-emissive only: an
+# emissive sphere makes the reference read the triangle buffer out of bounds (render_kernel.cpp:690-700).
+SPH_MAIN = [0.3275, 0.7, 0.3725, 0.2, 0, 0, 0, 1.0, 0.71, 0.29, 1.0, 0.4]  # main.cpp:72 (commented out there)
+SPH_DIFFUSE = [-0.35, 0.3, 0.1, 0.25, 0, 0, 0, 0.2, 0.6, 0.9, 0.0, 0.8]
+SPH_DRAGON = [[2.6, 1.0, 1.4, 1.0, 0, 0, 0, 0.95, 0.95, 0.95, 1.0, 0.1],
+              [-2.9, 0.8, 0.6, 0.8, 0, 0, 0, 0.8, 0.3, 0.2, 0.0, 0.6]]
+
+# (name, scene, sky, camera, W, H, spp, bounces, pixels or None for full frame, mat override[, spheres])
 RENDERS = [
     ("cfg1_cornell12", "cornell12", "S", "cornell", 256, 256, 4, 3, None, None),
     ("cornell32_128", "cornell", "S", "cornell", 128, 128, 4, 3, None, None),
@@ -38,7 +46,17 @@ RENDERS = [
     (f"cfg5_sweep_m{mi}_r{ri}", "dragon", "L", "dragon", 1920, 1080, 1024, 8, 48,
      (1, [0.0, 1.0 / 3.0, 2.0 / 3.0, 1.0][mi], [0.05, 0.25, 0.5, 1.0][ri]))
     for mi in range(4) for ri in range(4)
+] + [
+    ("spheres_cornell32_128", "cornell", "S", "cornell", 128, 128, 4, 3, None, None, [SPH_MAIN]),
+    ("spheres_cornell32_64spp", "cornell", "S", "cornell", 256, 256, 64, 8, 1024, None, [SPH_MAIN, SPH_DIFFUSE]),
+    ("spheres_dragon", "dragon", "L", "dragon", 1920, 1080, 64, 8, 1024, None, SPH_DRAGON),
 ]
+
+
+def sphere_env(spheres):
+    """RT_SPHERES for ref_driver: the float32 values as C99 hex floats (exact through strtof)."""
+    f32 = np.asarray(spheres, np.float32).reshape(-1, 12)
+    return ";".join(",".join(float(v).hex() for v in row) for row in f32)
 
 
 def run(*args, env=None):
@@ -132,12 +150,15 @@ def main():
     np.savez_compressed(os.path.join(OUT, "rays_dragon.npz"), rays=rays, hits=hits)
 
     # renders
-    for name, sc, sk, cam, W, H, spp, nb, npx, mo in RENDERS:
+    for name, sc, sk, cam, W, H, spp, nb, npx, mo, *rest in RENDERS:
         obj = scenes.scene_path(sc)
-        env = {"RT_MAT_OVERRIDE": f"{mo[0]}:{mo[1]!r}:{mo[2]!r}"} if mo else None
+        env = {"RT_MAT_OVERRIDE": f"{mo[0]}:{mo[1]!r}:{mo[2]!r}"} if mo else {}
         entry = {"scene": sc, "sky": sk, "camera": cam, "W": W, "H": H, "spp": spp, "bounces": nb}
         if mo:
             entry["mat_override"] = {"index": mo[0], "metalness": mo[1], "roughness": mo[2]}
+        if rest:
+            env["RT_SPHERES"] = sphere_env(rest[0])
+            entry["spheres"] = np.asarray(rest[0], np.float32).reshape(-1, 12).tolist()
         if npx is None:
             out = os.path.join(tmp, "fb.f32")
             log = run("render", obj, sky[sk], cam, W, H, spp, nb, out, env=env)
