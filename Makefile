@@ -77,3 +77,15 @@ variant: $(OBJ)/rt_scene.host.o $(OBJ)/rt_imageio.host.o $(OBJ)/rt_capi_host.hos
 	@mkdir -p $(LIB)
 	$(HIPCC) $(HIPFLAGS) $(DEFS) -c $(SRC)/rt_render.hip -o $(OBJ)/rt_render_$(V).o
 	$(HIPCC) -shared --offload-arch=$(ARCH) -fPIC $(OBJ)/rt_render_$(V).o $^ -o $(LIB)/librt_hip_$(V).so
+
+# C++ drop-in check (container only): include/render_kernel_hip.h against the
+# reference's headers and objects (oracle/_ref, `make ref`), linked to the hostsim
+# build of the C ABI. tests/test_shim.py runs it.
+REFDIR ?= /root/reference
+REFOBJ := oracle/_ref/objO2
+build/shim_test: tests/native/shim_test.cpp include/render_kernel_hip.h include/rt_hip.h $(LIB)/librt_hostsim.so
+	@mkdir -p build
+	$(CXX) -std=gnu++20 -O2 -fopenmp -Iinclude -I$(REFDIR)/include -I$(REFDIR)/rapidobj -I$(REFDIR) $< \
+	  $(REFOBJ)/bvh.o $(REFOBJ)/flattened_bvh.o $(REFOBJ)/triangle.o $(REFOBJ)/vec.o $(REFOBJ)/color.o \
+	  $(REFOBJ)/mat.o $(REFOBJ)/camera.o $(REFOBJ)/ray.o $(REFOBJ)/utils.o -Wl,--gc-sections \
+	  -L$(LIB) -lrt_hostsim -Wl,-rpath,'$$ORIGIN/../$(LIB)' -o $@

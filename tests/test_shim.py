@@ -1,0 +1,37 @@
+"""The C++ drop-in (include/render_kernel_hip.h) compiled against the
+REFERENCE's own headers and objects, driven as main.cpp drives
+render_kernel.h, linked to the hostsim build of the C ABI: the Cfg1 frame
+must equal the compiled reference's golden bit for bit, and in-place edits of
+the material vector between renders must behave as the reference's
+`const std::vector<SimpleMaterial>&` member does (render_kernel.h:81-93).
+Container only: needs /root/reference (skipped elsewhere)."""
+from __future__ import annotations
+
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import golden_io as gio
+import rt_cases
+import scenes
+
+REF = "/root/reference/include"
+
+
+@pytest.mark.skipif(not os.path.isdir(REF), reason="needs the reference's headers (container only)")
+def test_cpp_shim_renders_cfg1_bit_exact(manifest, tmp_path):
+    subprocess.run(["make", "-C", gio.REPO, "-s", "ref", "build/shim_test"], check=True)
+    e = rt_cases.golden_case("cfg1_cornell12", manifest)
+    sky = tmp_path / "sky.raw"
+    scenes.write_sky_raw(str(sky), e["sky"])
+    out = tmp_path / "fb.f32"
+    r = subprocess.run([os.path.join(gio.REPO, "build", "shim_test"), scenes.scene_path(e["scene"]), str(sky),
+                        e["camera"], str(e["W"]), str(e["H"]), str(e["spp"]), str(e["bounces"]), str(out)],
+                       capture_output=True, text=True)
+    print(r.stdout, r.stderr)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "materials_by_reference 1 changed 1 pixel 1" in r.stdout
+    fb = np.fromfile(out, dtype="<f4").reshape(e["H"], e["W"], 4)
+    np.testing.assert_array_equal(fb.view(np.uint32), e["expected"].view(np.uint32))
