@@ -4,6 +4,9 @@
 #include "rt_scene.h"
 
 #include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <thread>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -13,6 +16,32 @@
 #include <unordered_map>
 
 namespace rt {
+
+int worker_count()
+{
+    for (const char* v : {"RT_HOST_THREADS", "OMP_NUM_THREADS"})
+        if (const char* e = std::getenv(v))
+            if (int n = std::atoi(e); n > 0) return std::min(n, 256);
+    const unsigned hw = std::thread::hardware_concurrency();
+    return (int)std::max(1u, std::min(hw, 16u));
+}
+
+void parallel_for(int n, int workers, const std::function<void(int)>& fn)
+{
+    workers = std::max(1, std::min(workers, n));
+    if (workers == 1) {
+        for (int i = 0; i < n; i++) fn(i);
+        return;
+    }
+    std::atomic<int> next{0};
+    auto run = [&]() {
+        for (int i; (i = next.fetch_add(1)) < n;) fn(i);
+    };
+    std::vector<std::thread> th;
+    for (int w = 1; w < workers; w++) th.emplace_back(run);
+    run();
+    for (auto& t : th) t.join();
+}
 
 // ======================================================================= OBJ
 namespace {
@@ -25,12 +54,15 @@ struct MtlMat {
 
 bool read_file(const std::string& path, std::string& out)
 {
-    std::ifstream f(path, std::ios::binary);
+    FILE* f = std::fopen(path.c_str(), "rb");
     if (!f) return false;
-    std::ostringstream ss;
-    ss << f.rdbuf();
-    out = ss.str();
-    return true;
+    std::fseek(f, 0, SEEK_END);
+    const long n = std::ftell(f);
+    std::fseek(f, 0, SEEK_SET);
+    out.resize(n > 0 ? (size_t)n : 0);
+    const bool ok = n >= 0 && std::fread(&out[0], 1, out.size(), f) == out.size();
+    std::fclose(f);
+    return ok;
 }
 
 inline const char* skip_ws(const char* p, const char* e)
@@ -121,7 +153,7 @@ inline bool read_index(const char*& p, const char* e, int nverts, int& out)
 
 }  // namespace
 
-int load_obj(const std::string& path, Mesh& out, std::string& err)
+int load_obj_serial(const std::string& path, Mesh& out, std::string& err)
 {
     std::string text;
     if (!read_file(path, text)) {
@@ -229,6 +261,242 @@ int load_obj(const std::string& path, Mesh& out, std::string& err)
     return 0;
 }
 
+// Parallel form of load_obj_serial: the text is cut into chunks at line ends;
+// workers parse each chunk's vertex and face lines (faces keep their raw OBJ
+// indices and the chunk-local vertex count, for relative indices), the mtllib /
+// usemtl lines are replayed in file order on one thread (so a usemtl resolves
+// against the libraries loaded before it), and workers then emit each chunk's
+// triangles at their final offsets. The first error in file order is reported,
+// as the serial parse would stop there.
+namespace {
+struct ObjChunk {
+    const char *b, *e;
+    std::vector<float> verts;
+    std::vector<long> idx;         // raw OBJ indices of the chunk's faces, concatenated
+    std::vector<int> fsize, fvloc; // per face: vertex count, chunk-local vertex count before it
+    struct Ev {
+        int kind;  // 0 usemtl, 1 mtllib
+        int face;  // chunk-local face index it precedes
+        std::string name;
+    };
+    std::vector<Ev> ev;
+    size_t err_at = SIZE_MAX;  // byte offset of the first error
+    std::string err;
+    int err_code = 0;
+    // phase 2 results
+    size_t vbase = 0, tbase = 0;
+    bool live = false;  // at or before the first chunk with a parse error
+    std::vector<std::pair<int, int>> mat_at;  // (local face, material) transitions
+    int mat0 = -1;
+    std::vector<int> emissive;
+};
+}  // namespace
+
+int load_obj(const std::string& path, Mesh& out, std::string& err)
+{
+    std::string text;
+    if (!read_file(path, text)) {
+        err = "cannot read " + path;
+        return -1;
+    }
+    const int workers = worker_count();
+    size_t par_min = 4u << 20;  // (RT_OBJ_PARALLEL_MIN: tests force the chunked path on small files)
+    if (const char* e = std::getenv("RT_OBJ_PARALLEL_MIN")) par_min = (size_t)std::atol(e);
+    if (text.size() < par_min || workers < 2) return load_obj_serial(path, out, err);
+    out = Mesh();
+    const char* T = text.data();
+    const size_t N = text.size();
+    const int nch = 4 * workers;
+    std::vector<ObjChunk> ch(nch);
+    {
+        size_t pos = 0;
+        for (int c = 0; c < nch; c++) {
+            size_t end = c + 1 == nch ? N : std::max(pos, N * (c + 1) / nch);
+            while (end < N && T[end - 1] != '\n') end++;
+            ch[c].b = T + pos;
+            ch[c].e = T + end;
+            pos = end;
+        }
+    }
+    auto fail = [&](ObjChunk& C, const char* at, int code, const char* msg) {
+        if ((size_t)(at - T) < C.err_at) C.err_at = (size_t)(at - T), C.err = msg, C.err_code = code;
+    };
+    parallel_for(nch, workers, [&](int c) {
+        ObjChunk& C = ch[c];
+        const char* p = C.b;
+        while (p < C.e && C.err_at == SIZE_MAX) {
+            const char* le = (const char*)std::memchr(p, '\n', C.e - p);
+            if (!le) le = C.e;
+            const char* q = skip_ws(p, le);
+            if (q + 1 < le && q[0] == 'v' && (q[1] == ' ' || q[1] == '\t')) {
+                q += 1;
+                float v[3];
+                bool ok = true;
+                for (int i = 0; i < 3 && ok; i++) ok = read_float(q, le, v[i]);
+                if (!ok) {
+                    fail(C, p, -3, "bad vertex line");
+                    break;
+                }
+                C.verts.insert(C.verts.end(), v, v + 3);
+            } else if (q + 1 < le && q[0] == 'f' && (q[1] == ' ' || q[1] == '\t')) {
+                q += 1;
+                int n = 0;
+                for (;;) {
+                    const char* r = skip_ws(q, le);
+                    if (r >= le || *r == '\n' || *r == '#') break;
+                    char* end;
+                    const long v = std::strtol(r, &end, 10);
+                    if (end == r) break;
+                    q = end;
+                    while (q < le && *q != ' ' && *q != '\t' && *q != '\r') q++;  // skip /vt/vn
+                    C.idx.push_back(v);
+                    n++;
+                }
+                if (n < 3) {
+                    fail(C, p, -3, "face with fewer than 3 vertices");
+                    break;
+                }
+                if (n > 4) {
+                    fail(C, p, -4, "polygons with more than 4 vertices are not supported (rapidobj earcut path)");
+                    break;
+                }
+                C.fsize.push_back(n);
+                C.fvloc.push_back((int)(C.verts.size() / 3));
+            } else if (q + 6 < le && (std::strncmp(q, "usemtl", 6) == 0 || std::strncmp(q, "mtllib", 6) == 0) &&
+                       (q[6] == ' ' || q[6] == '\t')) {
+                const int kind = q[0] == 'u' ? 0 : 1;
+                q = skip_ws(q + 6, le);
+                std::string name(q, le);
+                while (!name.empty() && (name.back() == ' ' || name.back() == '\t' || name.back() == '\r')) name.pop_back();
+                C.ev.push_back({kind, (int)C.fsize.size(), std::move(name)});
+            }
+            p = le + 1;
+        }
+    });
+    // file order: offsets, materials (mtllib / usemtl replayed), the first parse error
+    std::vector<MtlMat> mtl;
+    std::unordered_map<std::string, int> names;
+    int cur = -1;
+    size_t vb = 0, tb = 0;
+    for (ObjChunk& C : ch) {
+        C.vbase = vb;
+        C.tbase = tb;
+        C.mat0 = cur;
+        C.live = true;
+        for (auto& ev : C.ev) {
+            if (ev.kind == 1) {
+                if (int r = load_mtl(dirname_of(path) + "/" + ev.name, mtl, names, err)) return r;
+            } else {
+                auto it = names.find(ev.name);
+                cur = it == names.end() ? -1 : it->second;
+                C.mat_at.push_back({ev.face, cur});
+            }
+        }
+        if (C.err_at != SIZE_MAX) break;  // nothing after the first error is needed
+        vb += C.verts.size() / 3;
+        for (int n : C.fsize) tb += n == 3 ? 1 : 2;
+    }
+    // (a parse error stops the serial loader there; faces before it may still fail the
+    // index check first, which the emit pass below reports by position)
+    size_t first_err = SIZE_MAX;
+    std::string first_msg;
+    int first_code = 0;
+    for (ObjChunk& C : ch)
+        if (C.err_at != SIZE_MAX) {
+            first_err = C.err_at, first_msg = C.err, first_code = C.err_code;
+            break;
+        }
+    std::vector<float> pos(3 * vb);
+    out.tris.resize(9 * tb);
+    out.mat_idx.resize(tb);
+    parallel_for(nch, workers, [&](int c) {
+        const ObjChunk& C = ch[c];
+        if (C.live && C.vbase * 3 + C.verts.size() <= pos.size())
+            std::memcpy(pos.data() + 3 * C.vbase, C.verts.data(), C.verts.size() * 4);
+    });
+    std::vector<size_t> idx_err(nch, SIZE_MAX);
+    parallel_for(nch, workers, [&](int c) {
+        ObjChunk& C = ch[c];
+        if (!C.live) return;  // (past the first parse error)
+        size_t t = C.tbase, o = 0;
+        size_t m = 0;
+        int mat = C.mat0;
+        for (size_t f = 0; f < C.fsize.size(); f++) {
+            while (m < C.mat_at.size() && C.mat_at[m].first <= (int)f) mat = C.mat_at[m++].second;
+            const int n = C.fsize[f];
+            const long nv = (long)(C.vbase + C.fvloc[f]);
+            int face[4];
+            bool bad = false;
+            for (int k = 0; k < n; k++) {
+                const long v = C.idx[o + k];
+                face[k] = v > 0 ? (int)(v - 1) : (int)(nv + v);
+                if (face[k] < 0 || face[k] >= nv) bad = true;
+            }
+            o += n;
+            if (bad) {
+                idx_err[c] = f;
+                return;
+            }
+            if (t + (n == 3 ? 1 : 2) > tb) return;  // (the chunk holding the parse error: faces past tb)
+            auto emit = [&](int i0, int i1, int i2) {
+                const int id[3] = {i0, i1, i2};
+                for (int k = 0; k < 3; k++) std::memcpy(&out.tris[9 * t + 3 * k], &pos[3 * (size_t)id[k]], 12);
+                out.mat_idx[t] = mat + 1;  // utils.cpp:51-56
+                if (mat >= 0) {
+                    const float* ke = mtl[mat].ke;
+                    if (ke[0] > 0 || ke[1] > 0 || ke[2] > 0) C.emissive.push_back((int)t);  // utils.cpp:58-69
+                }
+                t++;
+            };
+            if (n == 3) {
+                emit(face[0], face[1], face[2]);
+            } else {  // rapidobj::Triangulate quad rule (rapidobj.hpp:7164-7225), as load_obj_serial
+                const float* P0 = &pos[3 * (size_t)face[0]];
+                const float* P1 = &pos[3 * (size_t)face[1]];
+                const float* P2 = &pos[3 * (size_t)face[2]];
+                const float* P3 = &pos[3 * (size_t)face[3]];
+                float e02x = P0[0] - P2[0], e02y = P0[1] - P2[1], e02z = P0[2] - P2[2];
+                float e13x = P1[0] - P3[0], e13y = P1[1] - P3[1], e13z = P1[2] - P3[2];
+                float d02 = e02x * e02x + e02y * e02y + e02z * e02z;
+                float d13 = e13x * e13x + e13y * e13y + e13z * e13z;
+                bool less = d02 < d13;
+                emit(face[0], face[1], less ? face[2] : face[3]);
+                emit(less ? face[0] : face[1], face[2], face[3]);
+            }
+        }
+    });
+    for (int c = 0; c < nch; c++) {
+        // an out-of-range index in chunk c comes before any parse error in a later chunk
+        if (ch[c].err_at != SIZE_MAX && idx_err[c] == SIZE_MAX) break;
+        if (idx_err[c] != SIZE_MAX) {
+            err = "face index out of range";
+            return -3;
+        }
+        if (ch[c].err_at != SIZE_MAX) break;
+    }
+    if (first_err != SIZE_MAX) {
+        err = first_msg;
+        return first_code;
+    }
+    for (const ObjChunk& C : ch) out.emissive.insert(out.emissive.end(), C.emissive.begin(), C.emissive.end());
+    // SimpleMaterial list (utils.cpp:73-95)
+    auto push_mat = [&](float er, float eg, float eb, float dr, float dg, float db, float metal, float rough) {
+        const float mm[10] = {er, eg, eb, 1.0f, dr, dg, db, 1.0f, metal, rough};
+        out.mats.insert(out.mats.end(), mm, mm + 10);
+    };
+    push_mat(1.0f, 0.0f, 1.0f, 0.0f, 0.0f, 0.0f, 0.0f, 1.0f);
+    for (const MtlMat& m : mtl) {
+        float rough = std::max(1.0e-2f, m.pr);
+        float metal = m.pm;
+        if (m.illum == 0) {
+            rough = 1.0f;
+            metal = 0.0f;
+        }
+        push_mat(m.ke[0], m.ke[1], m.ke[2], m.kd[0], m.kd[1], m.kd[2], metal, rough);
+    }
+    return 0;
+}
+
 // ==================================================================== octree
 namespace {
 
@@ -239,6 +507,18 @@ const float PN[7][3] = {{1, 0, 0},   {0, 1, 0},    {0, 0, 1},   {S3, S3, S3},
 inline float pdot(int i, const float* p) { return PN[i][0] * p[0] + PN[i][1] * p[1] + PN[i][2] * p[2]; }
 inline float fmin_(float a, float b) { return (b < a) ? b : a; }  // std::min
 inline float fmax_(float a, float b) { return (a < b) ? b : a; }  // std::max
+
+void root_box(const float* tris, int ntris, float* mn, float* mx)  // bvh.cpp:19-37
+{
+    for (int k = 0; k < 3; k++) mn[k] = INFINITY, mx[k] = -INFINITY;
+    for (int t = 0; t < ntris; t++)
+        for (int j = 0; j < 3; j++)
+            for (int k = 0; k < 3; k++) {
+                float v = tris[9 * (size_t)t + 3 * j + k];
+                mn[k] = fmin_(mn[k], v);
+                mx[k] = fmax_(mx[k], v);
+            }
+}
 
 struct Builder {
     const float* T;
@@ -290,6 +570,41 @@ struct Builder {
             }
         } else
             insert_to_children(ni, id, depth);
+    }
+    // Top-down form of the insertions for node ni at `depth` receiving ids[0..n)
+    // (ascending): the same tree insert() builds from the same ids in order (see
+    // build_octree). The ids are partitioned stably in place, tmp[0..n) is scratch.
+    void build_from(int ni, int32_t* ids, int n, int32_t* tmp, int depth, const float* cen)
+    {
+        const bool exceeded = t.max_depth != -1 && depth == t.max_depth;
+        if (exceeded || n <= t.leaf_max) {
+            t.pool[ni].tris.assign(ids, ids + n);
+            return;
+        }
+        t.pool[ni].leaf = false;
+        create_children(ni);
+        const OctNode& nd = t.pool[ni];
+        const float m0 = (nd.mn[0] + nd.mx[0]) / 2, m1 = (nd.mn[1] + nd.mx[1]) / 2, m2 = (nd.mn[2] + nd.mx[2]) / 2;
+        int cnt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        for (int i = 0; i < n; i++) {
+            const float* c = cen + 3 * (size_t)ids[i];
+            const int o = (c[0] > m0 ? 1 : 0) + (c[1] > m1 ? 2 : 0) + (c[2] > m2 ? 4 : 0);
+            tmp[i] = o;
+            cnt[o]++;
+        }
+        int off[9];
+        off[0] = 0;
+        for (int o = 0; o < 8; o++) off[o + 1] = off[o] + cnt[o];
+        int pos[8];
+        for (int o = 0; o < 8; o++) pos[o] = off[o];
+        for (int i = 0; i < n; i++) {  // stable scatter into tmp, then back
+            const int o = tmp[i];
+            tmp[i] = ids[i] | (o << 28);  // (ids < 2^28: checked by the caller)
+        }
+        for (int i = 0; i < n; i++) ids[pos[tmp[i] >> 28]++] = tmp[i] & 0x0fffffff;
+        int kids[8];
+        for (int o = 0; o < 8; o++) kids[o] = t.pool[ni].child[o];
+        for (int o = 0; o < 8; o++) build_from(kids[o], ids + off[o], cnt[o], tmp + off[o], depth + 1, cen);
     }
     void insert_to_children(int ni, int id, int depth)  // bvh.h:109-125
     {
@@ -346,25 +661,163 @@ struct Builder {
 
 }  // namespace
 
-void build_octree(const float* tris, int ntris, int max_depth, int leaf_max, Octree& out)
+// Serial build: the reference's insertion order, one triangle at a time (bvh.cpp:52-60).
+void build_octree_serial(const float* tris, int ntris, int max_depth, int leaf_max, Octree& out)
 {
     out.pool.clear();
     out.pool.reserve((size_t)ntris / 2 + 16);
     out.max_depth = max_depth;
     out.leaf_max = leaf_max;
-    // BVH::BVH (bvh.cpp:19-37): root box from the vertex min / max
-    float mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
-    for (int t = 0; t < ntris; t++)
-        for (int j = 0; j < 3; j++)
-            for (int k = 0; k < 3; k++) {
-                float v = tris[9 * (size_t)t + 3 * j + k];
-                mn[k] = fmin_(mn[k], v);
-                mx[k] = fmax_(mx[k], v);
-            }
+    float mn[3], mx[3];
+    root_box(tris, ntris, mn, mx);
     Builder b(tris, out);
     b.new_node(mn, mx);
     for (int id = 0; id < ntris; id++) b.insert(0, id, 0);  // bvh.cpp:52-60
     b.compute_volume(0);
+}
+
+// Parallel build, identical tree. With insertion in id order (bvh.cpp:52-60), a
+// node receives exactly the triangles whose centroids route to it through its
+// ancestors' (fixed) boxes; it splits iff more than leaf_max of them arrive
+// below max_depth; and its list is in ascending id order (a split re-inserts the
+// list in order, later ids are larger). So the octree is built top-down: a node's
+// ascending id list is partitioned (stably) into its 8 children's, and subtrees
+// below the first levels are built on worker threads into their own pools. Leaf
+// volumes fold their triangles in list order and internal volumes their children
+// 0..7, as bvh.h:55-65 does, so the planes are the same floats.
+void build_octree(const float* tris, int ntris, int max_depth, int leaf_max, Octree& out)
+{
+    out.pool.clear();
+    out.max_depth = max_depth;
+    out.leaf_max = leaf_max;
+    const int workers = worker_count();
+    if (ntris < 65536 || workers < 2 || ntris >= (1 << 28)) {
+        build_octree_serial(tris, ntris, max_depth, leaf_max, out);
+        return;
+    }
+    auto T0 = std::chrono::steady_clock::now();
+    auto lap = [&](const char* what) {
+        if (!std::getenv("RT_BUILD_TIMES")) return;
+        auto T1 = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "[octree] %s %.1f ms\n", what, std::chrono::duration<double, std::milli>(T1 - T0).count());
+        T0 = T1;
+    };
+    // Triangle::bbox_centroid (triangle.cpp:3-6), as insert_to_children computes it
+    std::vector<float> cen(3 * (size_t)ntris);
+    parallel_for(workers, workers, [&](int w) {
+        const int b = (int)((long)ntris * w / workers), e = (int)((long)ntris * (w + 1) / workers);
+        for (int id = b; id < e; id++) {
+            const float* a = tris + 9 * (size_t)id;
+            for (int k = 0; k < 3; k++) {
+                float lo = fmin_(a[k], fmin_(a[3 + k], a[6 + k]));
+                float hi = fmax_(a[k], fmax_(a[3 + k], a[6 + k]));
+                cen[3 * (size_t)id + k] = (1.f / 2) * (lo + hi);
+            }
+        }
+    });
+    struct Sub {
+        int node;  // pool slot of the subtree root (in the top pool)
+        int depth;
+        std::vector<int32_t> ids;
+        Octree part;  // the subtree, built by a worker
+    };
+    Builder top(tris, out);
+    float mn[3], mx[3];
+    root_box(tris, ntris, mn, mx);
+    top.new_node(mn, mx);
+    std::vector<int32_t> all(ntris);
+    for (int i = 0; i < ntris; i++) all[i] = i;
+    // expand the top levels breadth-first until there are enough subtrees to share out
+    std::vector<Sub> frontier;
+    frontier.push_back(Sub{0, 0, std::move(all), {}});
+    const size_t want = 16 * (size_t)workers;
+    for (int level = 0; level < 6 && frontier.size() < want; level++) {
+        std::vector<Sub> next;
+        bool grew = false;
+        for (Sub& sb : frontier) {
+            OctNode& n = out.pool[sb.node];
+            const bool exceeded = max_depth != -1 && sb.depth == max_depth;
+            if (exceeded || (int)sb.ids.size() <= leaf_max) {
+                next.push_back(std::move(sb));
+                continue;
+            }
+            n.leaf = false;
+            top.create_children(sb.node);
+            const OctNode& nn = out.pool[sb.node];
+            const float m0 = (nn.mn[0] + nn.mx[0]) / 2, m1 = (nn.mn[1] + nn.mx[1]) / 2, m2 = (nn.mn[2] + nn.mx[2]) / 2;
+            std::vector<int32_t> parts[8];
+            for (int id : sb.ids) {
+                const float* c = &cen[3 * (size_t)id];
+                const int o = (c[0] > m0 ? 1 : 0) + (c[1] > m1 ? 2 : 0) + (c[2] > m2 ? 4 : 0);
+                parts[o].push_back(id);
+            }
+            for (int o = 0; o < 8; o++) next.push_back(Sub{out.pool[sb.node].child[o], sb.depth + 1, std::move(parts[o]), {}});
+            grew = true;
+        }
+        frontier.swap(next);
+        if (!grew) break;
+    }
+    lap("centroids + top levels");
+    // subtrees on the workers, largest first
+    std::vector<int> order(frontier.size());
+    for (size_t i = 0; i < order.size(); i++) order[i] = (int)i;
+    std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return frontier[a].ids.size() > frontier[b].ids.size(); });
+    parallel_for((int)order.size(), workers, [&](int j) {
+        Sub& sb = frontier[order[j]];
+        Octree& part = sb.part;
+        part.max_depth = max_depth;
+        part.leaf_max = leaf_max;
+        part.pool.reserve(sb.ids.size() / 2 + 16);
+        Builder b(tris, part);
+        const OctNode& r = out.pool[sb.node];
+        b.new_node(r.mn, r.mx);
+        std::vector<int32_t> tmp(sb.ids.size());
+        b.build_from(0, sb.ids.data(), (int)sb.ids.size(), tmp.data(), sb.depth, cen.data());
+        b.compute_volume(0);
+    });
+    lap("subtrees");
+    // graft the subtrees into the top pool (their roots replace the frontier slots):
+    // part node i > 0 of subtree j -> base[j] + i - 1, moved by the workers
+    std::vector<size_t> base(frontier.size() + 1);
+    base[0] = out.pool.size();
+    for (size_t j = 0; j < frontier.size(); j++) base[j + 1] = base[j] + frontier[j].part.pool.size() - 1;
+    out.pool.resize(base[frontier.size()]);
+    parallel_for((int)frontier.size(), workers, [&](int j) {
+        Sub& sb = frontier[j];
+        std::vector<OctNode>& pp = sb.part.pool;
+        auto remap = [&](OctNode& n) {
+            if (!n.leaf)
+                for (int i = 0; i < 8; i++) n.child[i] = n.child[i] == 0 ? sb.node : (int32_t)(base[j] + n.child[i] - 1);
+        };
+        for (size_t i = 1; i < pp.size(); i++) {
+            remap(pp[i]);
+            out.pool[base[j] + i - 1] = std::move(pp[i]);
+        }
+        remap(pp[0]);
+        out.pool[sb.node] = std::move(pp[0]);
+        std::vector<OctNode>().swap(pp);
+    });
+    lap("graft");
+    // volumes of the top levels (their frontier children are done)
+    std::vector<int> st;
+    std::vector<int> post;
+    st.push_back(0);
+    std::vector<char> is_front(out.pool.size(), 0);
+    for (const Sub& sb : frontier) is_front[sb.node] = 1;
+    while (!st.empty()) {
+        const int n = st.back();
+        st.pop_back();
+        if (is_front[n] || out.pool[n].leaf) continue;
+        post.push_back(n);
+        for (int i = 0; i < 8; i++) st.push_back(out.pool[n].child[i]);
+    }
+    for (size_t i = post.size(); i-- > 0;) {
+        OctNode& nd = out.pool[post[i]];
+        for (int c = 0; c < 8; c++) {
+            const OctNode& ch = out.pool[nd.child[c]];
+            for (int p = 0; p < 7; p++) nd.dn[p] = fmin_(nd.dn[p], ch.dn[p]), nd.df[p] = fmax_(nd.df[p], ch.df[p]);
+        }
+    }
 }
 
 std::vector<char> dump_octree(const Octree& t)
@@ -533,8 +986,61 @@ void pad_box(const Box& b, float* mn, float* mx)
 struct SahBuilder {
     std::vector<Prim>& P;
     std::vector<BvhNode>& nodes;
-    std::vector<int32_t> order;  // leaf order of P indices
+    int workers = 1;
+    static constexpr int kParMin = 1 << 15;  // ranges binned by the workers (top levels)
     explicit SahBuilder(std::vector<Prim>& p, std::vector<BvhNode>& n) : P(p), nodes(n) {}
+
+    // centroid bins of [b, e) on one axis (min / max merges: any chunk order gives the same boxes)
+    void bin(int ax, int b, int e, float lo, float sc, Box* bb, int* cnt) const
+    {
+        for (int i = 0; i < kBins; i++) bb[i].reset(), cnt[i] = 0;
+        auto run = [&](int cb, int ce, Box* xb, int* xc) {  // (bins in locals: no false sharing)
+            Box lb[kBins];
+            int lc[kBins] = {0};
+            for (auto& x : lb) x.reset();
+            for (int i = cb; i < ce; i++) {
+                const int bi = std::min(kBins - 1, (int)((P[i].c[ax] - lo) * sc));
+                lc[bi]++;
+                lb[bi].grow(P[i].b);
+            }
+            for (int i = 0; i < kBins; i++) xb[i] = lb[i], xc[i] = lc[i];
+        };
+        if (e - b < kParMin || workers < 2) {
+            run(b, e, bb, cnt);
+            return;
+        }
+        const int nch = workers;
+        std::vector<Box> pb((size_t)nch * kBins);
+        std::vector<int> pc((size_t)nch * kBins, 0);
+        for (auto& x : pb) x.reset();
+        parallel_for(nch, workers, [&](int c) {
+            run(b + (int)((long)(e - b) * c / nch), b + (int)((long)(e - b) * (c + 1) / nch), &pb[(size_t)c * kBins],
+                &pc[(size_t)c * kBins]);
+        });
+        for (int c = 0; c < nch; c++)
+            for (int i = 0; i < kBins; i++) bb[i].grow(pb[(size_t)c * kBins + i]), cnt[i] += pc[(size_t)c * kBins + i];
+    }
+
+    void bounds(int b, int e, Box& bb, Box& cb) const
+    {
+        bb.reset();
+        cb.reset();
+        if (e - b < kParMin || workers < 2) {
+            for (int i = b; i < e; i++) bb.grow(P[i].b), cb.grow(P[i].c);
+            return;
+        }
+        std::vector<Box> xb(workers), xc(workers);
+        parallel_for(workers, workers, [&](int c) {
+            Box lb, lc;
+            lb.reset();
+            lc.reset();
+            const int cb0 = b + (int)((long)(e - b) * c / workers), ce = b + (int)((long)(e - b) * (c + 1) / workers);
+            for (int i = cb0; i < ce; i++) lb.grow(P[i].b), lc.grow(P[i].c);
+            xb[c] = lb;
+            xc[c] = lc;
+        });
+        for (int c = 0; c < workers; c++) bb.grow(xb[c]), cb.grow(xc[c]);
+    }
 
     // Splits [b, e) in place; returns the split point or -1 for a leaf.
     int split(int b, int e, const Box& cb)
@@ -547,14 +1053,9 @@ struct SahBuilder {
             const float lo = cb.mn[ax], ext = cb.mx[ax] - cb.mn[ax];
             if (!(ext > 0.0f)) continue;
             Box bb[kBins];
-            int cnt[kBins] = {0};
-            for (auto& x : bb) x.reset();
+            int cnt[kBins];
             const float sc = kBins / ext;
-            for (int i = b; i < e; i++) {
-                int bi = std::min(kBins - 1, (int)((P[i].c[ax] - lo) * sc));
-                cnt[bi]++;
-                bb[bi].grow(P[i].b);
-            }
+            bin(ax, b, e, lo, sc, bb, cnt);
             float rarea[kBins];
             int rcnt[kBins];
             Box acc;
@@ -590,20 +1091,52 @@ struct SahBuilder {
         return mid;
     }
 
+    struct Task {
+        int b, e, node, side;  // side: 0 left child slot, 1 right child slot of `node`
+    };
+
+    // One task of the depth-first build into `nd`: fills the slot, pushes the children.
+    void process(std::vector<BvhNode>& nd, const Task& t, std::vector<Task>& st)
+    {
+        BvhNode& parent = nd[t.node];
+        float* mn = t.side ? parent.rmin : parent.lmin;
+        float* mx = t.side ? parent.rmax : parent.lmax;
+        int32_t& ref = t.side ? parent.right : parent.left;
+        int32_t& cnt = t.side ? parent.rcount : parent.lcount;
+        if (t.e <= t.b) {  // empty slot (count -1): never entered
+            for (int i = 0; i < 3; i++) mn[i] = INFINITY, mx[i] = -INFINITY;
+            ref = 0;
+            cnt = -1;
+            return;
+        }
+        Box bb, cb;
+        bounds(t.b, t.e, bb, cb);
+        pad_box(bb, mn, mx);
+        const int m = split(t.b, t.e, cb);
+        if (m < 0) {
+            ref = t.b;  // leaf entries are P[t.b .. t.e) in final order
+            cnt = t.e - t.b;
+            return;
+        }
+        const int ni = (int)nd.size();
+        ref = ni;
+        cnt = 0;
+        nd.push_back(BvhNode{});  // (invalidates `parent`; not used below)
+        st.push_back({m, t.e, ni, 1});
+        st.push_back({t.b, m, ni, 0});
+    }
+
+    // Top levels here (their binning on the workers), then the subtrees below
+    // `cutoff` primitives on the workers into their own node arrays, grafted back.
+    // The tree (splits, leaf order of P) is the serial build's; only the binary
+    // node numbering differs, which collapse_bvh4 (depth-first) does not see.
     void run()
     {
+        auto T00 = std::chrono::steady_clock::now();
         const int n = (int)P.size();
-        struct Task {
-            int b, e, node, side;  // side: 0 left child slot, 1 right child slot of `node`
-        };
         nodes.clear();
         nodes.push_back(BvhNode{});
         std::vector<Task> st;
-        auto bounds = [&](int b, int e, Box& bb, Box& cb) {
-            bb.reset();
-            cb.reset();
-            for (int i = b; i < e; i++) bb.grow(P[i].b), cb.grow(P[i].c);
-        };
         // root: split the whole set into the root node's two children
         Box bb, cb;
         bounds(0, n, bb, cb);
@@ -611,34 +1144,63 @@ struct SahBuilder {
         if (mid < 0) mid = n;  // tiny scene: one leaf in the left slot, empty right
         st.push_back({mid, n, 0, 1});
         st.push_back({0, mid, 0, 0});
+        const int cutoff = (workers > 1 && n >= 65536) ? std::max(4096, n / (3 * workers)) : -1;
+        std::vector<Task> deferred;
         while (!st.empty()) {
             const Task t = st.back();
             st.pop_back();
-            BvhNode& parent = nodes[t.node];
-            float* mn = t.side ? parent.rmin : parent.lmin;
-            float* mx = t.side ? parent.rmax : parent.lmax;
-            int32_t& ref = t.side ? parent.right : parent.left;
-            int32_t& cnt = t.side ? parent.rcount : parent.lcount;
-            if (t.e <= t.b) {  // empty slot (count -1): never entered
-                for (int i = 0; i < 3; i++) mn[i] = INFINITY, mx[i] = -INFINITY;
-                ref = 0;
-                cnt = -1;
+            if (t.e - t.b <= cutoff && t.e - t.b > kLeafMax) {
+                deferred.push_back(t);
                 continue;
             }
-            bounds(t.b, t.e, bb, cb);
-            pad_box(bb, mn, mx);
-            const int m = split(t.b, t.e, cb);
-            if (m < 0) {
-                ref = t.b;  // leaf entries are P[t.b .. t.e) in final order
-                cnt = t.e - t.b;
-                continue;
+            process(nodes, t, st);
+        }
+        auto T0 = std::chrono::steady_clock::now();
+        if (std::getenv("RT_BUILD_TIMES"))
+            std::fprintf(stderr, "[sah] top %.1f ms: %zu nodes, %zu deferred (cutoff %d)\n",
+                         std::chrono::duration<double, std::milli>(T0 - T00).count(), nodes.size(), deferred.size(), cutoff);
+        if (deferred.empty()) return;
+        std::vector<std::vector<BvhNode>> local(deferred.size());
+        std::vector<int> order(deferred.size());
+        for (size_t i = 0; i < order.size(); i++) order[i] = (int)i;
+        std::stable_sort(order.begin(), order.end(), [&](int x, int y) {
+            return deferred[x].e - deferred[x].b > deferred[y].e - deferred[y].b;
+        });
+        parallel_for((int)deferred.size(), workers, [&](int j) {
+            const int k = order[j];
+            std::vector<BvhNode>& nd = local[k];
+            nd.push_back(BvhNode{});  // local 0: stands in for the task's parent
+            std::vector<Task> ls{{deferred[k].b, deferred[k].e, 0, deferred[k].side}};
+            while (!ls.empty()) {
+                const Task t = ls.back();
+                ls.pop_back();
+                process(nd, t, ls);
             }
-            const int ni = (int)nodes.size();
-            ref = ni;
-            cnt = 0;
-            nodes.push_back(BvhNode{});  // (invalidates `parent`; not used below)
-            st.push_back({m, t.e, ni, 1});
-            st.push_back({t.b, m, ni, 0});
+        });
+        if (std::getenv("RT_BUILD_TIMES"))
+            std::fprintf(stderr, "[sah] subtrees %.1f ms\n",
+                         std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - T0).count());
+        for (size_t k = 0; k < deferred.size(); k++) {
+            const std::vector<BvhNode>& nd = local[k];
+            const int base = (int)nodes.size() - 1;  // local i > 0 -> base + i
+            auto fix = [&](int32_t& ref, int32_t cnt) {
+                if (cnt == 0) ref += base;
+            };
+            for (size_t i = 1; i < nd.size(); i++) {
+                BvhNode x = nd[i];
+                fix(x.left, x.lcount);
+                fix(x.right, x.rcount);
+                nodes.push_back(x);
+            }
+            BvhNode& p = nodes[deferred[k].node];
+            const BvhNode& v = nd[0];
+            if (deferred[k].side) {
+                std::memcpy(p.rmin, v.rmin, 12), std::memcpy(p.rmax, v.rmax, 12);
+                p.right = v.right + (v.rcount == 0 ? base : 0), p.rcount = v.rcount;
+            } else {
+                std::memcpy(p.lmin, v.lmin, 12), std::memcpy(p.lmax, v.lmax, 12);
+                p.left = v.left + (v.lcount == 0 ? base : 0), p.lcount = v.lcount;
+            }
         }
     }
 };
@@ -717,6 +1279,13 @@ static void collapse_bvh4(const std::vector<BvhNode>& b2, std::vector<Bvh4Node>&
 
 void build_search_bvh(FlatBvh& out)
 {
+    auto T0 = std::chrono::steady_clock::now();
+    auto lap = [&](const char* what) {
+        if (!std::getenv("RT_BUILD_TIMES")) return;
+        auto T1 = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "[search bvh] %s %.1f ms\n", what, std::chrono::duration<double, std::milli>(T1 - T0).count());
+        T0 = T1;
+    };
     // plane nesting along every parent link (enables rt_fast.h's one-test chain check)
     out.chain_monotone = true;
     for (size_t r = 1; r < out.nodes.size() && out.chain_monotone; r++) {
@@ -727,7 +1296,9 @@ void build_search_bvh(FlatBvh& out)
     }
     const int n = (int)(out.tri4.size() / 3);
     std::vector<Prim> P(n);
-    for (int k = 0; k < n; k++) {
+    const int nw = worker_count();
+    parallel_for(nw, nw, [&](int w) {
+    for (int k = (int)((long)n * w / nw); k < (int)((long)n * (w + 1) / nw); k++) {
         const float4_* r = &out.tri4[3 * (size_t)k];
         const float a[3] = {r[0].x, r[0].y, r[0].z};
         // vertices as the reference's Triangle holds them: b = a + e1, c = a + e2
@@ -741,10 +1312,15 @@ void build_search_bvh(FlatBvh& out)
         for (int i = 0; i < 3; i++) P[k].c[i] = 0.5f * (P[k].b.mn[i] + P[k].b.mx[i]);
         P[k].k = k;
     }
+    });
+    lap("chain check + prims");
     SahBuilder B(P, out.bvh);
+    B.workers = worker_count();
     if (n > 0) B.run();
+    lap("SAH build");
     out.bvh_tri4.resize(3 * (size_t)n);
-    for (int i = 0; i < n; i++) {
+    parallel_for(nw, nw, [&](int w) {
+    for (int i = (int)((long)n * w / nw); i < (int)((long)n * (w + 1) / nw); i++) {
         const int k = P[i].k;
         out.bvh_tri4[3 * (size_t)i] = out.tri4[3 * (size_t)k];
         std::memcpy(&out.bvh_tri4[3 * (size_t)i].w, &k, 4);
@@ -753,13 +1329,16 @@ void build_search_bvh(FlatBvh& out)
         out.bvh_tri4[3 * (size_t)i + 2] = out.tri4[3 * (size_t)k + 2];
         out.bvh_tri4[3 * (size_t)i + 2].w = out.tri4[3 * (size_t)k].w;  // original triangle index (brute-force ties)
     }
+    });
     if (out.bvh.empty()) {  // no triangles: a root with two empty slots
         BvhNode r{};
         for (int i = 0; i < 3; i++) r.lmin[i] = r.rmin[i] = INFINITY, r.lmax[i] = r.rmax[i] = -INFINITY;
         r.lcount = r.rcount = -1;
         out.bvh.push_back(r);
     }
+    lap("leaf records");
     collapse_bvh4(out.bvh, out.bvh4);
+    lap("collapse");
 }
 
 // ======================================================================= env

@@ -11,6 +11,7 @@
 #pragma once
 
 #include <cstdint>
+#include <functional>
 #include <string>
 #include <vector>
 
@@ -28,7 +29,8 @@ struct Mesh {
 
 // Parses an OBJ (+ its mtllib) like Utils::parse_obj. Returns 0 or a negative
 // error; `err` receives a message.
-int load_obj(const std::string& path, Mesh& out, std::string& err);
+int load_obj(const std::string& path, Mesh& out, std::string& err);       // chunks parsed by the workers
+int load_obj_serial(const std::string& path, Mesh& out, std::string& err);  // one pass, file order
 
 // ---------------------------------------------------------------- octree
 struct OctNode {
@@ -44,7 +46,16 @@ struct Octree {
     int max_depth = 32, leaf_max = 8;
 };
 
+// Parallel over worker threads (build_octree, rt_scene.cpp), the same tree as the
+// reference's one-triangle-at-a-time insertion (build_octree_serial).
 void build_octree(const float* tris, int ntris, int max_depth, int leaf_max, Octree& out);
+void build_octree_serial(const float* tris, int ntris, int max_depth, int leaf_max, Octree& out);
+
+// Host worker threads for scene preparation: OMP_NUM_THREADS / RT_HOST_THREADS if
+// set, else the hardware threads (at most 16: a GPU box's CPU share).
+int worker_count();
+// fn(task) for task in [0, n) on up to `workers` threads (dynamic, one task at a time).
+void parallel_for(int n, int workers, const std::function<void(int)>& fn);
 // Pre-order dump identical to oracle/ref/ref_driver.cpp "bvh".
 std::vector<char> dump_octree(const Octree& t);
 // Inverse of dump_octree: rebuilds an Octree from a caller's pre-order walk
