@@ -97,6 +97,10 @@ struct RtSceneView {
     const float4_* bvh_tri4;   // 3 records per triangle in BVH leaf order: {a.xyz, k}, {e1, leaf record}, {e2}
     const int32_t* parent;     // octree record -> parent record (-1 for the root)
     const int32_t* leaf_of;    // leaf-order triangle k -> its octree leaf record
+    // top of the search BVH: nodes [0, bvh4_ntop) are its first levels in breadth-first
+    // order (rt_scene.cpp bvh4_top_first). A kernel that stages them in LDS (rt_quad.h
+    // top_nodes_stage) sets bvh4_top in its own copy of the view; 0: read from memory.
+    int32_t bvh4_ntop, bvh4_top;
 };
 
 struct RtCamera {
@@ -123,5 +127,7 @@ enum {
     RT_STAT_ANY_LEAF,
     RT_STAT_VERIFY,    // octree slab tests of the verification walks
     RT_STAT_FALLBACK,  // queries answered by the exact octree walk
+    RT_STAT_QUAD_VISITS,  // k_trace: inner-node visits of the quad walks (one per quad trip)
+    RT_STAT_WAVE_SLOTS,   // k_trace: per 16-query chunk, 16 x its longest walk's visits (SIMT slots)
     RT_STAT_COUNT
 };

@@ -72,6 +72,43 @@ struct QuadStack {
     __device__ __forceinline__ void set_rec(int i, uint32_t rv) { r[i * QPB] = rv; }
 };
 
+// LDS-staged top of the search BVH: the first RT_TOP_NODES nodes (breadth-first,
+// rt_scene.cpp bvh4_top_first), copied once per block; every walk starts there,
+// so its first trips read LDS instead of L2.
+// Measured on cfg2 (r02): 0 / 21 / 32 / 64 nodes: 676 / 676 / 675 / 666 Msamples/s (the
+// top levels stay L2-resident anyway), so it is off by default.
+#ifndef RT_TOP_NODES
+#define RT_TOP_NODES 0
+#endif
+__device__ __forceinline__ float4_* top_nodes()
+{
+    __shared__ float4_ s_top[RT_TOP_NODES > 0 ? RT_TOP_NODES * 8 : 1];
+    return s_top;
+}
+// Copies the top nodes (whole block; ends with a barrier) and returns the count staged.
+__device__ __forceinline__ int top_nodes_stage(const RtSceneView& S)
+{
+    const int n = min(S.bvh4_ntop, RT_TOP_NODES);
+    float4_* t = top_nodes();
+    const float4_* g = (const float4_*)S.bvh4;
+    for (int i = (int)threadIdx.x; i < 8 * n; i += (int)blockDim.x) t[i] = g[i];
+    __syncthreads();
+    return n;
+}
+// Lane sub's 32-B child record of inner node `node` (LDS when staged).
+__device__ __forceinline__ void child_record(const RtSceneView& S, int node, int sub, float4_& a, float4_& b)
+{
+    if (RT_TOP_NODES > 0 && node < S.bvh4_top) {
+        const float4_* q = top_nodes() + 8 * node + 2 * sub;
+        a = q[0];
+        b = q[1];
+    } else {
+        const float4_* p = (const float4_*)(S.bvh4 + node) + 2 * sub;
+        a = p[0];
+        b = p[1];
+    }
+}
+
 // Lane `sub`'s child of inner node `node`: box test within [0, tmax].
 struct QChild {
     int item;  // node index or leaf item (rt_fast.h leaf_item)
@@ -80,8 +117,8 @@ struct QChild {
 };
 __device__ __forceinline__ QChild quad_child(const RtSceneView& S, int node, int sub, const RayB& rb, float tmax)
 {
-    const float4_* p = (const float4_*)(S.bvh4 + node) + 2 * sub;
-    const float4_ a = p[0], b = p[1];
+    float4_ a, b;
+    child_record(S, node, sub, a, b);
     rt_pin(a);
     rt_pin(b);
     const int ref = (int)rt_asuint(b.z), cnt = (int)rt_asuint(b.w);
@@ -355,6 +392,193 @@ __device__ int quad_query_any(const RtSceneView& S, V3 o, V3 d, QSTK& stk, int s
     }
 }
 
+// The whole-walk loops above, cut at trip boundaries and specialized by kind
+// (ANY: quad_query_any's visit order and answer; else quad_closest's), so that
+// k_trace can start a quad on its next query the moment its walk ends. One call
+// is one trip: the same loads, tests and stack moves as one iteration of those
+// loops, so the visits and answers are theirs.
+struct QState {
+    V3 o, d;
+    RayB rb;
+    FastHit h;
+    int sp, cur;
+};
+
+// false: the answer is already known (a NaN ray: no hit), no trip needed.
+template <bool ANY>
+__device__ __forceinline__ bool qstate_begin(QState& q, V3 o, V3 d, int sub, Stats* st)
+{
+    if (st && sub == 0) st->c[ANY ? RT_STAT_ANY_RAYS : RT_STAT_RAYS]++;
+    q.o = o;
+    q.d = d;
+    q.h.t = __builtin_inff();
+    q.h.t2 = __builtin_inff();
+    q.h.k = ANY ? 0 : -1;
+    q.h.leaf = -1;
+    q.h.prim = 0x7fffffff;
+    q.h.tie = false;
+    q.h.ovf = false;
+    if (rt_isnan(d.x) || rt_isnan(d.y) || rt_isnan(d.z) || rt_isnan(o.x) || rt_isnan(o.y) || rt_isnan(o.z)) {
+        q.h.t = -1.0f;
+        return false;
+    }
+    q.rb = rayb_setup(o, d);
+    q.sp = 0;
+    q.cur = 0;
+    return true;
+}
+
+// One trip. 0: go on; 1: the walk is over (ANY: q.h.k = 1 occluded / 0 not; else the
+// closest-hit record in q.h, to quad_closest_answer); -1: the bounded stack overflowed.
+#ifndef RT_VISIT_DESCEND
+#define RT_VISIT_DESCEND 2  // inner-node trips a quad_visit call may take in a row before returning
+                            // (cfg2, refill 8: 1 / 2 / 4 -> 680 / 725 / 706 Msamples/s)
+#endif
+template <bool ANY, class QSTK>
+__device__ __forceinline__ int quad_visit(const RtSceneView& S, QState& q, QSTK& stk, int sub, Stats* st)
+{
+    FastHit& h = q.h;
+#pragma unroll 1
+    for (int dd = 0; dd < RT_VISIT_DESCEND && q.cur >= 0; dd++) {
+        if (st && sub == 0) st->c[ANY ? RT_STAT_ANY_VOL : RT_STAT_VOL] += 4;
+        const float tmax = ANY ? __builtin_inff() : h.t + h.t * RT_T2_WINDOW;
+        const QChild c = quad_child(S, q.cur, sub, q.rb, tmax);
+        if (ANY) {
+            const int okb = c.ok ? 1 : 0;
+            const int o1 = qdpp<RT_QX1>(okb), o2 = qdpp<RT_QX2>(okb), o3 = qdpp<RT_QX3>(okb);
+            const int pre = (s_lower(sub, 1) ? o1 : 0) + (s_lower(sub, 2) ? o2 : 0) + (s_lower(sub, 3) ? o3 : 0);
+            const int nv = okb + o1 + o2 + o3;
+            if (q.sp + nv - 1 > QSTK::CAP) return -1;
+            if (c.ok && pre > 0) stk.set(q.sp + pre - 1, (uint32_t)c.item, 0.0f);
+            if (nv > 0) {
+                q.sp += nv - 1;
+                q.cur = qor(c.ok && pre == 0 ? c.item : 0);
+                continue;
+            }
+        } else {
+            const float key = c.ok ? c.tn : __builtin_inff();
+            const float k1 = qdppf<RT_QX1>(key), k2 = qdppf<RT_QX2>(key), k3 = qdppf<RT_QX3>(key);
+            const int s1 = sub ^ 1, s2 = sub ^ 2, s3 = sub ^ 3;
+            const int rank = (k1 < key || (k1 == key && s1 < sub) ? 1 : 0) + (k2 < key || (k2 == key && s2 < sub) ? 1 : 0) +
+                             (k3 < key || (k3 == key && s3 < sub) ? 1 : 0);
+            const int nv = qsum(c.ok ? 1 : 0);
+            if (q.sp + nv - 1 > QSTK::CAP) return -1;
+            if (c.ok && rank > 0) stk.set(q.sp + nv - 1 - rank, (uint32_t)c.item, key);
+            if (nv > 0) {
+                q.sp += nv - 1;
+                q.cur = qor(c.ok && rank == 0 ? c.item : 0);
+                continue;
+            }
+        }
+        // no child hit: pop (below)
+        q.cur = 0x7ffffffe;
+        break;
+    }
+    if (q.cur >= 0 && q.cur != 0x7ffffffe) return 0;  // (descended RT_VISIT_DESCEND times; still inner)
+    if (q.cur < 0) {
+        if (st && sub == 0) st->c[ANY ? RT_STAT_ANY_TRI : RT_STAT_TRI] += ((~q.cur) & 3) + 1;
+        int k, leaf, prim;
+        const float tv = quad_tri(S, q.cur, sub, q.o, q.d, k, leaf, prim);
+        if (ANY) {
+            const int hitb = tv < __builtin_inff() ? 1 : 0;
+            if (S.brute) {
+                if (qor(hitb)) {
+                    h.k = 1;
+                    return 1;
+                }
+            } else {
+                const int h1 = qdpp<RT_QX1>(hitb), h2 = qdpp<RT_QX2>(hitb), h3 = qdpp<RT_QX3>(hitb);
+                const int l1 = qdpp<RT_QX1>(leaf), l2 = qdpp<RT_QX2>(leaf), l3 = qdpp<RT_QX3>(leaf);
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    const int x = j ^ sub;
+                    const int hj = x == 0 ? hitb : x == 1 ? h1 : x == 2 ? h2 : h3;
+                    if (!hj) continue;
+                    const int lj = x == 0 ? leaf : x == 1 ? l1 : x == 2 ? l2 : l3;
+                    if (quad_chain_ok(S, q.o, q.d, lj, false, 0.0f, sub, st)) {
+                        h.k = 1;
+                        return 1;
+                    }
+                }
+            }
+        } else {
+            float m1 = tv, m2 = __builtin_inff();
+            {
+                const float o1 = qdppf<RT_QX1>(m1), o2 = qdppf<RT_QX1>(m2);
+                const float n1 = __builtin_fminf(m1, o1), n2 = __builtin_fminf(__builtin_fmaxf(m1, o1), __builtin_fminf(m2, o2));
+                m1 = n1, m2 = n2;
+            }
+            {
+                const float o1 = qdppf<RT_QX2>(m1), o2 = qdppf<RT_QX2>(m2);
+                const float n1 = __builtin_fminf(m1, o1), n2 = __builtin_fminf(__builtin_fmaxf(m1, o1), __builtin_fminf(m2, o2));
+                m1 = n1, m2 = n2;
+            }
+            int pm = tv == m1 ? prim : 0x7fffffff;
+            pm = min(pm, qdpp<RT_QX1>(pm));
+            pm = min(pm, qdpp<RT_QX2>(pm));
+            const bool mine = tv == m1 && prim == pm;
+            if (m1 < h.t) {
+                h.t2 = __builtin_fminf(h.t, m2);
+                h.t = m1;
+                h.k = qor(mine ? k : 0);
+                h.leaf = qor(mine ? leaf : 0);
+                h.prim = pm;
+                h.tie = m2 == m1;
+            } else if (m1 == h.t && m1 < __builtin_inff()) {
+                h.tie = true;
+                h.t2 = m1;
+                if (pm < h.prim) {
+                    h.k = qor(mine ? k : 0);
+                    h.leaf = qor(mine ? leaf : 0);
+                    h.prim = pm;
+                }
+            } else {
+                h.t2 = __builtin_fminf(h.t2, m1);
+            }
+        }
+    }
+    if (ANY) {
+        if (q.sp == 0) return 1;  // (h.k = 0: not occluded)
+        q.cur = (int)stk.rec(--q.sp);
+        return 0;
+    }
+    const float tmax = h.t + h.t * RT_T2_WINDOW;
+    int nxt = 0x7fffffff;
+    while (q.sp > 0) {
+        --q.sp;
+        if (stk.key(q.sp) <= tmax) {
+            nxt = (int)stk.rec(q.sp);
+            break;
+        }
+    }
+    q.cur = nxt;
+    return nxt == 0x7fffffff ? 1 : 0;
+}
+
+// quad_query_closest's answer from a finished walk: true with (t, k), false when the
+// exact walk must answer.
+__device__ __forceinline__ bool quad_closest_answer(const RtSceneView& S, const QState& q, int sub, float& t_out,
+                                                    int& k_out, Stats* st)
+{
+    const FastHit& h = q.h;
+    if (h.k < 0) {
+        t_out = -1.0f;
+        k_out = -1;
+        return true;
+    }
+    if (S.brute) {
+        t_out = h.t;
+        k_out = h.k;
+        return true;
+    }
+    if (h.tie) return false;
+    const float t2 = __builtin_fminf(h.t2, h.t + h.t * RT_T2_WINDOW);
+    if (!quad_chain_ok(S, q.o, q.d, h.leaf, true, t2, sub, st)) return false;
+    t_out = h.t;
+    k_out = h.k;
+    return true;
+}
+
 // A quad walk as a state machine, one node or leaf visit per qwalk_step, so
 // that a wave can refill a quad with its next query the moment the quad's
 // walk ends instead of waiting for the wave's slowest walk (k_trace), and so
@@ -405,9 +629,7 @@ struct QVisit {
 __device__ __forceinline__ void qwalk_issue(const QWalk& w, const RtSceneView& S, int sub, QVisit& v)
 {
     if (w.cur >= 0) {
-        const float4_* p = (const float4_*)(S.bvh4 + w.cur) + 2 * sub;
-        v.x0 = p[0];
-        v.x1 = p[1];
+        child_record(S, w.cur, sub, v.x0, v.x1);
         rt_pin(v.x0);
         rt_pin(v.x1);
     } else {
@@ -443,14 +665,24 @@ __device__ int qwalk_consume(QWalk& w, const RtSceneView& S, QSTK& stk, int sub,
             c.item = cnt > 0 ? leaf_item(ref, cnt) : ref;
         }
         const float key = c.ok ? c.tn : __builtin_inff();
-        // rank by (key, lane): the nearest hit child has rank 0
-        const float k1 = qdppf<RT_QX1>(key), k2 = qdppf<RT_QX2>(key), k3 = qdppf<RT_QX3>(key);
-        const int s1 = sub ^ 1, s2 = sub ^ 2, s3 = sub ^ 3;
-        const int rank = (k1 < key || (k1 == key && s1 < sub) ? 1 : 0) + (k2 < key || (k2 == key && s2 < sub) ? 1 : 0) +
-                         (k3 < key || (k3 == key && s3 < sub) ? 1 : 0);
+        // closest: rank by (key, lane), the nearest hit child has rank 0; occlusion (order-free
+        // answer): the ok lanes in lane order, as quad_query_any (nearest-first measured slower)
+        int rank;
+        if (anyq) {
+            const int okb = c.ok ? 1 : 0;
+            const int o1 = qdpp<RT_QX1>(okb), o2 = qdpp<RT_QX2>(okb), o3 = qdpp<RT_QX3>(okb);
+            const int pre = (s_lower(sub, 1) ? o1 : 0) + (s_lower(sub, 2) ? o2 : 0) + (s_lower(sub, 3) ? o3 : 0);
+            const int nok = okb + o1 + o2 + o3;
+            rank = pre == 0 ? 0 : nok - pre;  // first ok lane next; the others pushed, the second on top
+        } else {
+            const float k1 = qdppf<RT_QX1>(key), k2 = qdppf<RT_QX2>(key), k3 = qdppf<RT_QX3>(key);
+            const int s1 = sub ^ 1, s2 = sub ^ 2, s3 = sub ^ 3;
+            rank = (k1 < key || (k1 == key && s1 < sub) ? 1 : 0) + (k2 < key || (k2 == key && s2 < sub) ? 1 : 0) +
+                   (k3 < key || (k3 == key && s3 < sub) ? 1 : 0);
+        }
         const int nv = qsum(c.ok ? 1 : 0);
         if (w.sp + nv - 1 > QSTK::CAP) return -1;
-        // far children on the stack, nearest of them on top
+        // far children on the stack, the next of them on top
         if (c.ok && rank > 0) stk.set(w.sp + nv - 1 - rank, (uint32_t)c.item, key);
         if (nv > 0) {
             w.sp += nv - 1;

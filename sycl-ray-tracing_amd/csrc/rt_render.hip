@@ -313,6 +313,10 @@ __global__ __launch_bounds__(256) void k_init(rtk::WaveView W)
 #define RT_LDS_CAP_ANY 16
 #define RT_REFILL 16
 #define RT_QSTACK 32            // quad walks (rt_quad.h): stack entries per quad (item + key, 64 quads per block)
+#ifndef RT_TRACE_REFILL
+#define RT_TRACE_REFILL 4       // k_trace: idle quads of a wave that trigger a refill from its query stream (0: static
+                                // 16-query chunks). r02 sweep on cfg2 (RT_VISIT_DESCEND 2): 4 / 8 -> 726 / 723 vs 678 static
+#endif
 #ifndef RT_TRACE_OCC
 #define RT_TRACE_OCC 6          // k_trace waves per SIMD (8 fits the quad walks in 64 VGPRs but measured
                                 // 512 vs 539 Msamples/s: more trace waves crowd the other lanes k_step)
@@ -544,6 +548,81 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_STEP_OCC
     flush_stats<STATS>(st, stats);
 }
 
+// k_trace's fast roles with per-quad refill (RT_TRACE_REFILL > 0): see k_trace.
+template <bool ANY, bool STATS, class QSTK>
+__device__ __forceinline__ void trace_stream(const rtk::WaveView& W, const RtSceneView& S, QSTK& stk, const int* s_pre,
+                                             int first, int total, int wg, int wn, int32_t* fbn, rtk::RayRec* fbl,
+                                             rtk::Stats* ps)
+{
+    const int lane = lane_id(), qd = lane >> 2, sub = lane & 3;
+    int cursor = 0;                     // the wave's next stream position (uniform)
+    bool exhausted = wg * 16 >= total;  // (uniform)
+    bool active = false;
+    uint32_t target = 0;
+    rtk::QState q;
+    rtk::RayRec r;
+    for (;;) {
+        const unsigned long long bidle = __ballot(!active && sub == 0);
+        if (!exhausted && (__popcll(bidle) >= RT_TRACE_REFILL || bidle == 0x1111111111111111ull)) {
+            if (!active) {
+                const int j = cursor + __popcll(bidle & ((1ull << (qd * 4)) - 1ull));  // this quad's stream position
+                const int idx = (wg + (j >> 4) * wn) * 16 + (j & 15);
+                if (idx < total) {
+                    const int g = first + idx;
+                    const int seg = shard_find(s_pre, rtk::RK_COUNT * RT_QSHARDS, g);
+                    const int kind = seg / RT_QSHARDS;
+                    rtk::RayRec* qk = W.q[0];
+#pragma unroll
+                    for (int k2 = 1; k2 < rtk::RK_COUNT; k2++) qk = kind == k2 ? W.q[k2] : qk;
+                    r = qk[(size_t)(seg % RT_QSHARDS) * W.seg_cap + (g - s_pre[seg])];
+                    target = (rt_asuint(r.o.w) << 3) | (uint32_t)kind;
+                    if (forced_fallback(W, r.o, r.d)) {
+                        if (sub == 0) {
+                            r.d.w = rt_asfloat(target & 7u);
+                            fbl[atomicAdd(fbn, 1)] = r;
+                            atomicAdd(&W.r_park[target >> 3], 1);
+                        }
+                    } else if (rtk::qstate_begin<ANY>(q, rtk::v3of(r.o), rtk::v3of(r.d), sub, ps)) {
+                        active = true;
+                    } else if (sub == 0) {  // (a NaN ray: no hit)
+                        if (ANY)
+                            rtk::finish_any(W, target, false);
+                        else
+                            rtk::finish_closest(W, target, q.o, q.d, -1.0f, -1);
+                    }
+                }
+            }
+            cursor += __popcll(bidle);
+            exhausted = (wg + (cursor >> 4) * wn) * 16 >= total;
+        }
+        if (!__any(active)) {
+            if (exhausted) break;
+            continue;
+        }
+        if (active) {
+            int res = rtk::quad_visit<ANY>(S, q, stk, sub, ps);
+            if (res != 0) {
+                active = false;
+                float t = 0.0f;
+                int k = 0;
+                if (res > 0 && !ANY && !rtk::quad_closest_answer(S, q, sub, t, k, ps)) res = -1;
+                if (sub == 0) {
+                    if (res > 0) {
+                        if (ANY)
+                            rtk::finish_any(W, target, q.h.k == 1);
+                        else
+                            rtk::finish_closest(W, target, q.o, q.d, t, k);
+                    } else {  // the exact walk answers it (k_step(i))
+                        r.d.w = rt_asfloat(target & 7u);
+                        fbl[atomicAdd(fbn, 1)] = r;
+                        atomicAdd(&W.r_park[target >> 3], 1);
+                    }
+                }
+            }
+        }
+    }
+}
+
 template <bool STATS>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_OCC, 8))) void k_trace(rtk::WaveView W, int par, unsigned long long* stats)
 {
@@ -571,8 +650,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_OC
     rtk::Stats* ps = STATS ? &st : nullptr;
     const int b = (int)blockIdx.x;
 
+    // the search BVH's top levels in LDS (every walk's first trips)
+    RtSceneView S = W.S;
+    S.bvh4_top = rtk::top_nodes_stage(S);
     // fast roles: a quad of lanes per query (rt_quad.h), 16 queries per wave
-    const int sub = (int)(threadIdx.x & 3);
     rtk::QuadStack<RT_QSTACK, 64> stk{s_lds + (threadIdx.x >> 2), (float*)s_lds + RT_QSTACK * 64 + (threadIdx.x >> 2)};
     // queue segments (kind-major, then shard): prefix table in LDS
     shard_prefix(cnt, rtk::RK_COUNT * RT_QSHARDS,
@@ -592,6 +673,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_OC
     const int total = closest ? nc : na;
     int32_t* fbn = cnt + (closest ? C_FBC0 : C_FBA0) + par;  // walked exactly by k_step(i)
     rtk::RayRec* fbl = closest ? W.fb_c[par] : W.fb_a[par];
+#if RT_TRACE_REFILL
+    // The wave's queries are a stream (its 16-query chunks base = wg*16 + c*wn*16 in turn):
+    // each quad walks one, one trip per loop (rt_quad.h quad_visit), and as soon as
+    // RT_TRACE_REFILL quads are idle they all take the next queries, so a long walk holds
+    // up its own quad, not the wave's next 15 queries. Same trips and answers as the
+    // whole-walk functions.
+    if (closest)
+        trace_stream<false, STATS>(W, S, stk, s_pre, c0, total, wg, wn, fbn, fbl, ps);
+    else
+        trace_stream<true, STATS>(W, S, stk, s_pre, a0, total, wg, wn, fbn, fbl, ps);
+#else
+    const int sub = (int)(threadIdx.x & 3);
     for (int base = wg * 16; base < total; base += wn * 16) {
         const int idx = base + (lane_id() >> 2);
         bool fail = false;
@@ -621,13 +714,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_OC
             } else if (closest) {
                 float t;
                 int k;
-                if (rtk::quad_query_closest(W.S, rtk::v3of(r.o), rtk::v3of(r.d), stk, sub, t, k, ps)) {
+                if (rtk::quad_query_closest(S, rtk::v3of(r.o), rtk::v3of(r.d), stk, sub, t, k, ps)) {
                     if (sub == 0) rtk::finish_closest(W, target, rtk::v3of(r.o), rtk::v3of(r.d), t, k);
                 } else {
                     fail = sub == 0;
                 }
             } else {
-                const int a = rtk::quad_query_any(W.S, rtk::v3of(r.o), rtk::v3of(r.d), stk, sub, ps);
+                const int a = rtk::quad_query_any(S, rtk::v3of(r.o), rtk::v3of(r.d), stk, sub, ps);
                 if (a >= 0) {
                     if (sub == 0) rtk::finish_any(W, target, a == 1);
                 } else {
@@ -664,6 +757,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_OC
             }
         }
 #endif
+        if (STATS) {  // SIMT efficiency of the chunk: its quads' visits against 16 x the longest
+            int nv = idx < total && sub == 0 ? (int)((st.c[RT_STAT_VOL] + st.c[RT_STAT_ANY_VOL] - v0) / 4) : 0;
+            int vm = nv;
+            for (int o = 32; o > 0; o >>= 1) vm = max(vm, __shfl_xor(vm, o));
+            st.c[RT_STAT_QUAD_VISITS] += nv;
+            if (lane_id() == 0) st.c[RT_STAT_WAVE_SLOTS] += 16ull * vm;
+        }
         if (STATS && W.iterq && idx < total && sub == 0 && W.iter < RT_MAX_TIMED_ITERS) {
             // (RT_ITER_LOG: the longest walk of the launch in node visits, per role, and
             // how many walks took more than 24)
@@ -679,6 +779,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_OC
             atomicAdd(&W.r_park[target >> 3], 1);
         }
     }
+#endif
     flush_stats<STATS>(st, stats);
 }
 
@@ -712,6 +813,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TAIL_OCC
     int32_t* cnt = W.counters;
     shard_prefix(cnt, RT_QSHARDS, [&](int j) { return ac_at(par, j); }, s_pre);
     const int n = s_pre[RT_QSHARDS];
+    RtSceneView S = W.S;
+    S.bvh4_top = rtk::top_nodes_stage(S);
     rtk::Stats st;
     if (STATS)
         for (int i = 0; i < RT_STAT_COUNT; i++) st.c[i] = 0;
@@ -778,40 +881,66 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TAIL_OCC
         __builtin_amdgcn_wave_barrier();
 #if RT_TAIL_MIXED
         // trace: both lists in one index space, 16 queries (quads) per pass, each quad
-        // walking its own kind (quad_query_mixed): a step waits for its slowest query,
-        // not for the closest walk plus the occlusion walks after it
+        // walking its own kind a few trips per call (rt_quad.h quad_visit): a step waits
+        // for its slowest query, not for the closest walk plus the occlusion walks after it
         const int nq = nl[0] + nl[1];
         for (int base = 0; base < nq; base += 16) {
             const int qi = base + (lane >> 2);
+            bool act = false, exact = false;
+            int l = 0;
+            uint32_t target = 0;
+            rtk::QState q;
             if (qi < nq) {
-                const int l = qi < nl[0] ? 0 : 1;
+                l = qi < nl[0] ? 0 : 1;
                 const rtk::RayRec r = s_q[wv][l][l ? qi - nl[0] : qi];
-                const uint32_t target = rt_asuint(r.d.w);
-                const rtk::V3 o = rtk::v3of(r.o), d = rtk::v3of(r.d);
-                rtk::QWalk qw;
-                const int a = forced_fallback(W, r.o, r.d) ? -1 : rtk::quad_query_mixed(W.S, o, d, stk, sub, l == 1, qw, ps);
-                if (a >= 0 && sub == 0) {
-                    if (l == 0)
-                        rtk::finish_closest(W, target, o, d, qw.t, qw.k);
-                    else
-                        rtk::finish_any(W, target, qw.k == 1);
-                }
-                if (a < 0 && sub == 0) {  // the exact octree walk, to completion
-                    if (STATS) st.c[RT_STAT_FALLBACK]++;
-                    xs.f = stk;
-                    if (l == 0) {
-                        rtk::TravC T;
-                        if (rtk::travc_begin(W.S, T, o, d, ps))
-                            while (rtk::travc_step(W.S, T, xs, ps)) {
-                            }
-                        rtk::finish_closest(W, target, T.o, T.d, T.best_t, T.best_k);
-                    } else {
-                        rtk::TravA T;
-                        if (rtk::trava_begin(W.S, T, o, d, ps))
-                            while (rtk::trava_step(W.S, T, xs, ps)) {
-                            }
-                        rtk::finish_any(W, target, T.hit);
+                target = rt_asuint(r.d.w);
+                q.o = rtk::v3of(r.o);
+                q.d = rtk::v3of(r.d);
+                if (forced_fallback(W, r.o, r.d)) {
+                    exact = true;
+                } else {
+                    act = l ? rtk::qstate_begin<true>(q, q.o, q.d, sub, ps) : rtk::qstate_begin<false>(q, q.o, q.d, sub, ps);
+                    if (!act && sub == 0) {  // (a NaN ray: no hit)
+                        if (l == 0)
+                            rtk::finish_closest(W, target, q.o, q.d, -1.0f, -1);
+                        else
+                            rtk::finish_any(W, target, false);
                     }
+                }
+            }
+            while (__any(act)) {
+                if (act) {
+                    const int res = l ? rtk::quad_visit<true>(S, q, stk, sub, ps) : rtk::quad_visit<false>(S, q, stk, sub, ps);
+                    if (res != 0) {
+                        act = false;
+                        float t = 0.0f;
+                        int k = 0;
+                        const bool ok = res > 0 && (l == 1 || rtk::quad_closest_answer(S, q, sub, t, k, ps));
+                        if (ok && sub == 0) {
+                            if (l == 0)
+                                rtk::finish_closest(W, target, q.o, q.d, t, k);
+                            else
+                                rtk::finish_any(W, target, q.h.k == 1);
+                        }
+                        exact = !ok;
+                    }
+                }
+            }
+            if (exact && sub == 0) {  // the exact octree walk, to completion
+                if (STATS) st.c[RT_STAT_FALLBACK]++;
+                xs.f = stk;
+                if (l == 0) {
+                    rtk::TravC T;
+                    if (rtk::travc_begin(W.S, T, q.o, q.d, ps))
+                        while (rtk::travc_step(W.S, T, xs, ps)) {
+                        }
+                    rtk::finish_closest(W, target, T.o, T.d, T.best_t, T.best_k);
+                } else {
+                    rtk::TravA T;
+                    if (rtk::trava_begin(W.S, T, q.o, q.d, ps))
+                        while (rtk::trava_step(W.S, T, xs, ps)) {
+                        }
+                    rtk::finish_any(W, target, T.hit);
                 }
             }
         }
@@ -832,10 +961,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TAIL_OCC
                     if (l == 0) {
                         float t;
                         int k;
-                        fail = !rtk::quad_query_closest(W.S, o, d, stk, sub, t, k, ps);
+                        fail = !rtk::quad_query_closest(S, o, d, stk, sub, t, k, ps);
                         if (!fail && sub == 0) rtk::finish_closest(W, target, o, d, t, k);
                     } else {
-                        const int a = rtk::quad_query_any(W.S, o, d, stk, sub, ps);
+                        const int a = rtk::quad_query_any(S, o, d, stk, sub, ps);
                         fail = a < 0;
                         if (!fail && sub == 0) rtk::finish_any(W, target, a == 1);
                     }
@@ -933,6 +1062,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
                                                     float* __restrict__ out_t, int* __restrict__ out_k, int n)
 {
     __shared__ uint32_t s_lds[2 * RT_QSTACK * 64];
+    S.bvh4_top = rtk::top_nodes_stage(S);
     const int q = (int)(threadIdx.x >> 2), sub = (int)(threadIdx.x & 3);
     rtk::QuadStack<RT_QSTACK, 64> stk{s_lds + q, (float*)s_lds + RT_QSTACK * 64 + q};
     const int stride = (int)(gridDim.x * blockDim.x) >> 2;
@@ -1155,6 +1285,8 @@ int upload_one(rt_context* c, Backend* b, const std::vector<int32_t>& matk, bool
     v.bvh_tri4 = (const float4_*)b->bvh_tri4.p;
     v.parent = (const int32_t*)b->parent.p;
     v.leaf_of = (const int32_t*)b->leaf_of.p;
+    v.bvh4_ntop = c->flat.bvh4_ntop;
+    v.bvh4_top = 0;
     b->view = v;
     b->bl_rays = rt_scene_has_emissive_prim(c) ? 1 : 0;
     b->any_rays = v.n_spheres == 0 ? 1 : 0;

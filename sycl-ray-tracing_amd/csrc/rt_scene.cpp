@@ -1277,6 +1277,34 @@ static void collapse_bvh4(const std::vector<BvhNode>& b2, std::vector<Bvh4Node>&
     }
 }
 
+// Moves the first `k` nodes of a breadth-first walk of the 4-wide tree to the front
+// (in that order; the rest keep their depth-first order), so that the levels every
+// walk starts with are one contiguous block the kernels can stage in LDS. Returns
+// how many nodes that is.
+static int bvh4_top_first(std::vector<Bvh4Node>& b4, int k)
+{
+    const int n = (int)b4.size();
+    std::vector<int> bfs;
+    bfs.push_back(0);
+    for (size_t i = 0; i < bfs.size() && (int)bfs.size() < k; i++)
+        for (int c = 0; c < 4 && (int)bfs.size() < k; c++)
+            if (b4[bfs[i]].ch[c].cnt == 0) bfs.push_back(b4[bfs[i]].ch[c].ref);
+    std::vector<int> to(n, -1);
+    int next = 0;
+    for (int v : bfs) to[v] = next++;
+    for (int v = 0; v < n; v++)
+        if (to[v] < 0) to[v] = next++;
+    std::vector<Bvh4Node> out(n);
+    for (int v = 0; v < n; v++) {
+        Bvh4Node nd = b4[v];
+        for (auto& c : nd.ch)
+            if (c.cnt == 0) c.ref = to[c.ref];
+        out[to[v]] = nd;
+    }
+    b4.swap(out);
+    return (int)bfs.size();
+}
+
 void build_search_bvh(FlatBvh& out)
 {
     auto T0 = std::chrono::steady_clock::now();
@@ -1338,6 +1366,7 @@ void build_search_bvh(FlatBvh& out)
     }
     lap("leaf records");
     collapse_bvh4(out.bvh, out.bvh4);
+    out.bvh4_ntop = bvh4_top_first(out.bvh4, 256);
     lap("collapse");
 }
 

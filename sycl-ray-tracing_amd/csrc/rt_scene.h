@@ -73,7 +73,8 @@ struct FlatBvh {
     bool chain_monotone = false;  // every record's planes lie within its parent's
     // search BVH over tri4 (build_search_bvh)
     std::vector<BvhNode> bvh;    // binary SAH build
-    std::vector<Bvh4Node> bvh4;  // collapsed 4-wide form the device walks
+    std::vector<Bvh4Node> bvh4;  // collapsed 4-wide form the device walks (first bvh4_ntop: breadth-first top)
+    int bvh4_ntop = 0;
     std::vector<float4_> bvh_tri4;
 };
 void flatten_octree(const Octree& t, const float* tris, int ntris, FlatBvh& out);
