@@ -308,3 +308,24 @@ def test_gpu_parked_walks_small_launches(name, budget, every, tail, manifest, ca
     print(name, "fallbacks", st["fallback"], "in k_tail", st["tail_fallback"], "iterations", rk.last_iterations())
     assert st["fallback"] > 0
     assert_parity(got, e["expected"], min_bitwise=1.0)
+
+
+@pytest.mark.parametrize("name,off,stride", [("cfg3_dragon", 311, 400), ("cfg4_dragon4k", 1083, 1100)])
+def test_gpu_full_rows_at_256spp_match_oracle(name, off, stride, manifest, cameras):
+    """Cfg3 (1080p) and Cfg4 (4K) at their full 256 spp: whole image rows
+    rendered as a row shard on the GPU (rt_render_device, rows off + j*stride)
+    against the oracle on the same rows."""
+    from hip_mem import DeviceBuffer
+    e = rt_cases.golden_case(name, manifest)
+    rk, _ = rt_cases.make_kernel(e, cameras, hostsim=False)
+    rows = np.arange(off, e["H"], stride)
+    init = np.zeros((rows.size, e["W"], 4), np.float32)
+    init[..., 3] = 1.0
+    buf = DeviceBuffer(init.nbytes)
+    buf.upload(init)
+    rk.render_device(buf.ptr, off, stride, None)
+    got = buf.download(init.shape, np.float32)
+    xs, ys = np.meshgrid(np.arange(e["W"]), rows)
+    e["px"] = np.stack([xs.ravel(), ys.ravel()], 1).astype(np.int32)
+    want = rt_cases.run_oracle(e, cameras)
+    assert_parity(got.reshape(-1, 4), want, min_bitwise=1.0)
