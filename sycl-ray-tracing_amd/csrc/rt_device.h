@@ -129,5 +129,6 @@ enum {
     RT_STAT_FALLBACK,  // queries answered by the exact octree walk
     RT_STAT_QUAD_VISITS,  // k_trace: inner-node visits of the quad walks (one per quad trip)
     RT_STAT_WAVE_SLOTS,   // k_trace: per 16-query chunk, 16 x its longest walk's visits (SIMT slots)
+    RT_STAT_REFILLS,      // k_trace stream: refill rounds of the waves
     RT_STAT_COUNT
 };

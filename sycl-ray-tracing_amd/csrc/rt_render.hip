@@ -594,10 +594,15 @@ __device__ __forceinline__ void trace_stream(const rtk::WaveView& W, const RtSce
             }
             cursor += __popcll(bidle);
             exhausted = (wg + (cursor >> 4) * wn) * 16 >= total;
+            if (STATS && lane == 0) ps->c[RT_STAT_REFILLS]++;
         }
         if (!__any(active)) {
             if (exhausted) break;
             continue;
+        }
+        if (STATS) {  // SIMT slots of this trip: 16 quads, the active ones used
+            if (active && sub == 0) ps->c[RT_STAT_QUAD_VISITS]++;
+            if (lane == 0) ps->c[RT_STAT_WAVE_SLOTS] += 16;
         }
         if (active) {
             int res = rtk::quad_visit<ANY>(S, q, stk, sub, ps);
@@ -1392,7 +1397,12 @@ int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounces, cons
     const int threads = 256;
     // k_trace: wave-strided over 2 grid-fills; RT_TRACE_OCC blocks resident per CU (quad
     // walks: 6 waves/SIMD measured best, 423 vs 374 Msamples/s at 4 and 350 at 8)
-    const int trace_blocks = dev_cus * 2 * RT_TRACE_OCC;
+    // k_trace grid-fills (RT_TRACE_FILLS): with per-wave query streams one fill is best, a wave's
+    // stream is longer and its end (the last long walk) costs less; cfg2: 0.75 / 1 / 1.25 / 1.5 / 2 / 3
+    // -> 739 / 730-740 / 731 / 724 / 708-710 / 692 Msamples/s
+    double trace_fills = 1.0;
+    if (const char* e = getenv("RT_TRACE_FILLS")) trace_fills = std::max(0.25, atof(e));
+    const int trace_blocks = (int)(dev_cus * trace_fills * RT_TRACE_OCC);
     const bool S = c->stats_enabled;
     unsigned long long* stats = (unsigned long long*)b->stats.p;
     if (S) HIPCHK(c, hipMemsetAsync(b->stats.p, 0, b->stats.bytes, s));

@@ -24,3 +24,9 @@ run() { # name, rocprof args...
 }
 run trace --kernel-trace --stats --output-format csv rocpd || exit 1
 run pmc_fetch --pmc FETCH_SIZE || exit 1
+# occupancy / issue / wait counters of the same command (one pass each)
+if [ -n "$PMC_DETAIL" ]; then
+  run pmc_a --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU || exit 1
+  run pmc_b --pmc SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_SALU SQ_INST_CYCLES_VMEM_RD SQ_THREAD_CYCLES_VALU SQ_LEVEL_WAVES SQ_INSTS_BRANCH SQ_LDS_BANK_CONFLICT || exit 1
+  run pmc_c --pmc TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum GRBM_GUI_ACTIVE TCP_PENDING_STALL_CYCLES_sum || exit 1
+fi
