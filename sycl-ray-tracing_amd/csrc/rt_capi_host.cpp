@@ -57,6 +57,7 @@ RtSceneView rt_host_view(const rt_context* c)
     v.leaf_of = c->flat.leaf_of.data();
     v.bvh4_ntop = c->flat.bvh4_ntop;
     v.bvh4_top = 0;
+    v.tri_mat = 0;
     return v;
 }
 
@@ -245,12 +246,13 @@ int rt_set_env(rt_context* c, const float* px, int w, int h, int ch, const float
     const size_t n = (size_t)w * h;
     c->ew = w;
     c->eh = h;
-    c->env.resize(n);
-    for (size_t i = 0; i < n; i++) c->env[i] = float4_{px[ch * i], px[ch * i + 1], px[ch * i + 2], 0.0f};
     c->env_lum.resize(n);
     c->cdf.resize(n);
     rt::env_luminance_cdf(px, w, h, ch, c->env_lum.data(), c->cdf.data());
     if (cdf) c->cdf.assign(cdf, cdf + n);
+    // RGB + the texel's luminance in w: the env-map sample reads both with one 16-B load
+    c->env.resize(n);
+    for (size_t i = 0; i < n; i++) c->env[i] = float4_{px[ch * i], px[ch * i + 1], px[ch * i + 2], c->env_lum[i]};
     c->cdf_row.assign((size_t)((h + 15) & ~15), 0.0f);  // (padded: the fence search loads 16 at a time)
     for (int y = 0; y < h; y++) c->cdf_row[y] = c->cdf[(size_t)y * w + w - 1];
     rt::env_cdf_fences(c->cdf.data(), c->cdf_row.data(), w, h, c->cdf_fence);

@@ -101,6 +101,7 @@ struct RtSceneView {
     // order (rt_scene.cpp bvh4_top_first). A kernel that stages them in LDS (rt_quad.h
     // top_nodes_stage) sets bvh4_top in its own copy of the view; 0: read from memory.
     int32_t bvh4_ntop, bvh4_top;
+    int32_t tri_mat;  // 1: tri4[3k + 1].w holds the material index of leaf-order triangle k (device copy)
 };
 
 struct RtCamera {

@@ -1250,7 +1250,10 @@ int upload_one(rt_context* c, Backend* b, const std::vector<int32_t>& matk, bool
         b->bl_rays = rt_scene_has_emissive_prim(c) ? 1 : 0;
         return RT_OK;
     }
-    if ((r = upload(c, b->nodes, c->flat.nodes)) || (r = upload(c, b->tri4, c->flat.tri4)) ||
+    // device triangle records carry the material index in e1.w (rt_wave.h hit_from)
+    std::vector<float4_> tri4 = c->flat.tri4;
+    for (size_t k = 0; k < matk.size(); k++) std::memcpy(&tri4[3 * k + 1].w, &matk[k], 4);
+    if ((r = upload(c, b->nodes, c->flat.nodes)) || (r = upload(c, b->tri4, tri4)) ||
         (r = upload(c, b->prim2k, c->flat.prim2k)) || (r = upload(c, b->mat_idx, c->mat_idx)) ||
         (r = upload(c, b->mats, c->mats)) || (r = upload(c, b->emissive, c->emissive)) ||
         (r = upload(c, b->spheres, c->spheres)) || (r = upload(c, b->env, c->env)) ||
@@ -1292,6 +1295,7 @@ int upload_one(rt_context* c, Backend* b, const std::vector<int32_t>& matk, bool
     v.leaf_of = (const int32_t*)b->leaf_of.p;
     v.bvh4_ntop = c->flat.bvh4_ntop;
     v.bvh4_top = 0;
+    v.tri_mat = 1;
     b->view = v;
     b->bl_rays = rt_scene_has_emissive_prim(c) ? 1 : 0;
     b->any_rays = v.n_spheres == 0 ? 1 : 0;

@@ -73,6 +73,7 @@ struct Hit {
     float t;   // -1: none
     int k;     // leaf-order triangle index, or -2 - sphere index
     int prim;  // primitive id (triangle id or sphere prim)
+    int mi;    // material index when the triangle record carries it (RtSceneView::tri_mat), else -1
     V3 p, n;
 };
 
@@ -703,6 +704,14 @@ RT_HD Mat load_mat(const RtSceneView& S, int prim)
 RT_HD Mat load_mat_hit(const RtSceneView& S, int k, int prim)
 {
     const RtMat m = S.mats[(k >= 0 && S.matk) ? S.matk[k] : S.mat_idx[prim]];
+    return Mat{Col{m.er, m.eg, m.eb}, Col{m.dr, m.dg, m.db}, m.metalness, m.roughness};
+}
+// The material of a hit record (its material index already read with the triangle when
+// the device records carry it: one dependent load fewer).
+RT_HD Mat load_mat_of(const RtSceneView& S, const Hit& h)
+{
+    if (h.mi < 0) return load_mat_hit(S, h.k, h.prim);
+    const RtMat m = S.mats[h.mi];
     return Mat{Col{m.er, m.eg, m.eb}, Col{m.dr, m.dg, m.db}, m.metalness, m.roughness};
 }
 

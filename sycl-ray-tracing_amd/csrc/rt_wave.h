@@ -335,11 +335,14 @@ RT_HD bool hit_from(const RtSceneView& S, V3 o, V3 d, float t, int k, Hit& h)
     h.t = t;
     h.k = k;
     h.prim = -1;
+    h.mi = -1;
     if (k >= 0) {  // triangle (triangle.h:46-56)
-        const V3 e1 = ld3(S.tri4[3 * k + 1]), e2 = ld3(S.tri4[3 * k + 2]);
+        const float4_ r1 = S.tri4[3 * k + 1];
+        const V3 e1 = ld3(r1), e2 = ld3(S.tri4[3 * k + 2]);
         h.p = add(o, mul(t, d));
         h.n = normalize(cross(e1, e2));
         h.prim = (int)rt_asuint(S.tri4[3 * k].w);
+        if (S.tri_mat) h.mi = (int)rt_asuint(r1.w);
     } else if (k <= -2) {  // sphere (sphere.h:46-48)
         const float4_ s0 = S.spheres[2 * (-2 - k)];
         h.p = add(o, mul(t, d));
@@ -359,7 +362,7 @@ RT_HD void shade(const WaveView& W, int p, PathReg& P, const Hit& h, Emit& e, St
 {
     const RtSceneView& S = W.S;
     if (st) st->c[RT_STAT_MAT]++;
-    const Mat m = load_mat_hit(S, h.k, h.prim);
+    const Mat m = load_mat_of(S, h);
     const V3 rd = P.rd;
     uint32_t fl = PF_AUX;
 
@@ -430,10 +433,13 @@ RT_HD void shade(const WaveView& W, int p, PathReg& P, const Hit& h, Emit& e, St
         V3 dir = v3(-st_ * rt_cosf(phi), -ct_, -st_ * rt_sinf(phi));
         float cosine = dot(h.n, dir);
         if (cosine > 0.0f) {
-            float pdf = S.env_lum[y * S.ew + x] / total;
+            // the texel and its f64-evaluated luminance in one record (env.w = env_lum, rt_set_env)
+            if (st) st->c[RT_STAT_ENV]++;
+            const float4_ et = S.env[y * S.ew + x];
+            float pdf = et.w / total;
             pdf = (float)((double)((pdf * (float)S.ew) * (float)S.eh) /
                           (2.0 * 3.14159265358979323846 * 3.14159265358979323846 * (double)st_));
-            Col rad = env_texel(S, x, y, st);
+            const Col rad = Col{et.x, et.y, et.z};
             Col brdf = ct_brdf(m, dir, neg(rd), h.n);
             float bp = ct_pdf(m, neg(rd), dir, h.n);
             float mis = power_heuristic(pdf, bp);
@@ -516,7 +522,7 @@ RT_HD void resolve(const WaveView& W, int p, PathReg& P, Stats* st)
             float ca = rt_max(dot(nh.n, neg(sdir)), 0.0f);
             if (ca > 0.0f) {
                 if (st) st->c[RT_STAT_MAT]++;
-                const Mat mm = load_mat_hit(S, nh.k, nh.prim);
+                const Mat mm = load_mat_of(S, nh);
                 const Col e = mm.emission;
                 if (e.r > 0 || e.g > 0 || e.b > 0) {
                     float d2 = t * t;
