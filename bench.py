@@ -220,10 +220,15 @@ def main():
         have = torch.cuda.device_count()
         if have < n_gpus:
             fail(f"--gpus {n_gpus} but only {have} HIP device(s) visible")
+    # (RT_BENCH_DEVICE_MOD / RT_BENCH_BACKEND: rehearse the multi-process path with several ranks on one
+    # GPU and gloo; never set for a measurement)
+    if os.environ.get("RT_BENCH_DEVICE_MOD"):
+        local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        backend = os.environ.get("RT_BENCH_BACKEND", "nccl")
+        dist.init_process_group(backend, device_id=dev if backend == "nccl" else None)
 
     import rt_amd
     from rt_amd.dist import ShardedFrame
@@ -282,7 +287,8 @@ def main():
         if world > 1:
             dist.barrier()
         elapsed = time.perf_counter() - t_start
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64,
+                         device=dev if world == 1 or dist.get_backend() == "nccl" else "cpu")
         if world > 1:
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
@@ -312,7 +318,7 @@ def main():
         achieved = algo / (avg_ms * 1e-3) / 1e9
         roofline = {"bound": "hbm", "kernel": "k_trace", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                    "traffic": load_traffic(f"{args.config}_1lane"),
+                    "traffic": load_traffic(f"{args.config}_1lane") if (n_gpus == 1 and not args.sim_world) else None,
                     "measured": "1-lane render after the timed steps (one stream: launches do not overlap); "
                                 "HIP events around each launch",
                     "algo_bytes_per_launch": round(algo), "avg_launch_ms": round(avg_ms, 4),
@@ -348,7 +354,7 @@ def main():
         if single_process_multi:
             par = f"one process, rt_create_multi over {n_gpus} GPUs: rows y%{n_gpus} + RCCL scatter/gather"
         elif world > 1:
-            par = f"{world} processes (torchrun): rows y%{world} per GPU + RCCL gather"
+            par = f"{world} processes (torchrun): rows y%{world} per GPU + {dist.get_backend()} gather"
         else:
             par = "1 GPU"
         out = {

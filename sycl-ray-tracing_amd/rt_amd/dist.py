@@ -60,8 +60,13 @@ class ShardedFrame:
         there (None elsewhere)."""
         if self.world == 1:
             return self.shard[: self.rows]
-        parts = [torch.empty_like(self.shard) for _ in range(self.world)] if self.rank == dst else None
-        dist.gather(self.shard, parts, dst=dst, group=group)
+        src = self.shard
+        if src.is_cuda and dist.get_backend(group) == "gloo":  # (gloo gathers host tensors: rehearsals)
+            src = src.cpu()
+        parts = [torch.empty_like(src) for _ in range(self.world)] if self.rank == dst else None
+        dist.gather(src, parts, dst=dst, group=group)
+        if parts is not None and parts[0].device != self.device:
+            parts = [x.to(self.device) for x in parts]
         if self.rank != dst:
             return None
         full = torch.empty((self.H, self.W, 4), dtype=torch.float32, device=self.device)
