@@ -131,5 +131,7 @@ enum {
     RT_STAT_QUAD_VISITS,  // k_trace: inner-node visits of the quad walks (one per quad trip)
     RT_STAT_WAVE_SLOTS,   // k_trace: per 16-query chunk, 16 x its longest walk's visits (SIMT slots)
     RT_STAT_REFILLS,      // k_trace stream: refill rounds of the waves
+    RT_STAT_DRAIN_SLOTS,  // k_trace stream: the WAVE_SLOTS spent after the wave's stream ran out
+    RT_STAT_DRAIN_VISITS, // ... and the QUAD_VISITS among them
     RT_STAT_COUNT
 };

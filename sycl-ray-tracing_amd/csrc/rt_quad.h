@@ -402,6 +402,7 @@ struct QState {
     RayB rb;
     FastHit h;
     int sp, cur;
+    int bot;  // occlusion walks shared with other quads (k_trace drain): entries below bot were taken
 };
 
 // false: the answer is already known (a NaN ray: no hit), no trip needed.
@@ -425,6 +426,7 @@ __device__ __forceinline__ bool qstate_begin(QState& q, V3 o, V3 d, int sub, Sta
     q.rb = rayb_setup(o, d);
     q.sp = 0;
     q.cur = 0;
+    q.bot = 0;
     return true;
 }
 
@@ -538,7 +540,7 @@ __device__ __forceinline__ int quad_visit(const RtSceneView& S, QState& q, QSTK&
         }
     }
     if (ANY) {
-        if (q.sp == 0) return 1;  // (h.k = 0: not occluded)
+        if (q.sp <= q.bot) return 1;  // (h.k = 0: no occluder in this quad's part of the walk)
         q.cur = (int)stk.rec(--q.sp);
         return 0;
     }

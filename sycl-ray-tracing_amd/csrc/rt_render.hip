@@ -313,6 +313,9 @@ __global__ __launch_bounds__(256) void k_init(rtk::WaveView W)
 #define RT_LDS_CAP_ANY 16
 #define RT_REFILL 16
 #define RT_QSTACK 32            // quad walks (rt_quad.h): stack entries per quad (item + key, 64 quads per block)
+#ifndef RT_TRACE_STEAL
+#define RT_TRACE_STEAL 0        // occlusion walks shared by idle quads once a wave's stream has run out
+#endif
 #ifndef RT_TRACE_REFILL
 #define RT_TRACE_REFILL 4       // k_trace: idle quads of a wave that trigger a refill from its query stream (0: static
                                 // 16-query chunks). r02 sweep on cfg2 (RT_VISIT_DESCEND 2): 4 / 8 -> 726 / 723 vs 678 static
@@ -601,8 +604,8 @@ __device__ __forceinline__ void trace_stream(const rtk::WaveView& W, const RtSce
             continue;
         }
         if (STATS) {  // SIMT slots of this trip: 16 quads, the active ones used
-            if (active && sub == 0) ps->c[RT_STAT_QUAD_VISITS]++;
-            if (lane == 0) ps->c[RT_STAT_WAVE_SLOTS] += 16;
+            if (active && sub == 0) ps->c[exhausted ? RT_STAT_DRAIN_VISITS : RT_STAT_QUAD_VISITS]++;
+            if (lane == 0) ps->c[exhausted ? RT_STAT_DRAIN_SLOTS : RT_STAT_WAVE_SLOTS] += 16;
         }
         if (active) {
             int res = rtk::quad_visit<ANY>(S, q, stk, sub, ps);
@@ -628,11 +631,162 @@ __device__ __forceinline__ void trace_stream(const rtk::WaveView& W, const RtSce
     }
 }
 
+// k_trace's occlusion role with cooperative drains (RT_TRACE_STEAL): as trace_stream<true>,
+// and once the wave's stream has run out an idle quad takes the OLDEST stack entry of a
+// walk that still has two or more and walks that subtree for it (the occlusion answer
+// does not depend on the visit order): an occluder found by either ends both; the walk
+// is over when its own part and every helper are done. Per quad in LDS (s_coop[8 * qd]):
+// 0 bottom of its stack (entries below were taken), 1 helpers working for it, 2 found
+// (1 occluded, 2 abort: a helper's stack overflowed), 3..8 its ray.
+template <bool STATS, class QSTK>
+__device__ __forceinline__ void trace_stream_any_coop(const rtk::WaveView& W, const RtSceneView& S, QSTK& stk,
+                                                      const int* s_pre, int first, int total, int wg, int wn,
+                                                      int32_t* fbn, rtk::RayRec* fbl, int* s_coop, rtk::Stats* ps)
+{
+    const int lane = lane_id(), qd = lane >> 2, sub = lane & 3;
+    const int bq = (int)(threadIdx.x >> 2);  // block quad index: LDS stack column and s_coop record
+    const int wq0 = bq & ~15;                 // the wave's first block quad
+    int* me = s_coop + 8 * bq;
+    int cursor = 0;                     // the wave's next stream position (uniform)
+    bool exhausted = wg * 16 >= total;  // (uniform)
+    int role = 0;                       // 0 idle, 1 walking its own query, 2 helping quad `vq`
+    bool waiting = false;               // own part done, helpers still out
+    int vq = 0;
+    uint32_t target = 0;
+    rtk::QState q;
+    rtk::RayRec r;
+    for (;;) {
+        const unsigned long long bidle = __ballot(role == 0 && sub == 0);
+        if (!exhausted && (__popcll(bidle) >= RT_TRACE_REFILL || bidle == 0x1111111111111111ull)) {
+            if (role == 0) {
+                const int j = cursor + __popcll(bidle & ((1ull << (qd * 4)) - 1ull));
+                const int idx = (wg + (j >> 4) * wn) * 16 + (j & 15);
+                if (idx < total) {
+                    const int g = first + idx;
+                    const int seg = shard_find(s_pre, rtk::RK_COUNT * RT_QSHARDS, g);
+                    const int kind = seg / RT_QSHARDS;
+                    rtk::RayRec* qk = W.q[0];
+#pragma unroll
+                    for (int k2 = 1; k2 < rtk::RK_COUNT; k2++) qk = kind == k2 ? W.q[k2] : qk;
+                    r = qk[(size_t)(seg % RT_QSHARDS) * W.seg_cap + (g - s_pre[seg])];
+                    target = (rt_asuint(r.o.w) << 3) | (uint32_t)kind;
+                    if (forced_fallback(W, r.o, r.d)) {
+                        if (sub == 0) {
+                            r.d.w = rt_asfloat(target & 7u);
+                            fbl[atomicAdd(fbn, 1)] = r;
+                            atomicAdd(&W.r_park[target >> 3], 1);
+                        }
+                    } else if (rtk::qstate_begin<true>(q, rtk::v3of(r.o), rtk::v3of(r.d), sub, ps)) {
+                        role = 1;
+                        waiting = false;
+                        if (sub == 0) {
+                            me[0] = 0;
+                            me[1] = 0;
+                            me[2] = 0;
+                            me[3] = (int)rt_asuint(r.o.x), me[4] = (int)rt_asuint(r.o.y), me[5] = (int)rt_asuint(r.o.z);
+                            me[6] = (int)rt_asuint(r.d.x), me[7] = (int)rt_asuint(r.d.y);
+                        }
+                        if (sub == 1) s_coop[8 * 64 + bq] = (int)rt_asuint(r.d.z);
+                    } else if (sub == 0) {
+                        rtk::finish_any(W, target, false);
+                    }
+                }
+            }
+            cursor += __popcll(bidle);
+            exhausted = (wg + (cursor >> 4) * wn) * 16 >= total;
+            if (STATS && lane == 0) ps->c[RT_STAT_REFILLS]++;
+        }
+        // cooperative drain: idle quads take the oldest entry of a walk with two or more left
+        if (exhausted) {
+            const unsigned long long bfree = __ballot(role == 0 && sub == 0);
+            const bool can = role == 1 && !waiting && q.sp - me[0] >= 2;
+            const unsigned long long bvict = __ballot(can && sub == 0);
+            if (bfree && bvict) {
+                if (role == 0) {
+                    const int i = __popcll(bfree & ((1ull << (qd * 4)) - 1ull));  // this free quad's rank
+                    if (i < __popcll(bvict)) {
+                        unsigned long long v = bvict;
+                        for (int k = 0; k < i; k++) v &= v - 1;
+                        vq = wq0 + (__ffsll((long long)v) - 1) / 4;  // the i-th victim's block quad
+                        int* vr = s_coop + 8 * vq;
+                        const int bot = vr[0];
+                        const int item = (int)stk.r[bot * 64 + vq - bq];  // (QuadStack column of quad vq)
+                        q.o = rtk::v3(rt_asfloat((uint32_t)vr[3]), rt_asfloat((uint32_t)vr[4]), rt_asfloat((uint32_t)vr[5]));
+                        q.d = rtk::v3(rt_asfloat((uint32_t)vr[6]), rt_asfloat((uint32_t)vr[7]),
+                                      rt_asfloat((uint32_t)s_coop[8 * 64 + vq]));
+                        q.rb = rtk::rayb_setup(q.o, q.d);
+                        q.h.k = 0;
+                        q.sp = 0;
+                        q.bot = 0;
+                        q.cur = item;
+                        role = 2;
+                        if (sub == 0) {
+                            vr[0] = bot + 1;        // (one helper per walk and trip: no race)
+                            atomicAdd(&vr[1], 1);   // (helpers of the walk may finish in this trip)
+                        }
+                    }
+                }
+            }
+        }
+        const unsigned long long bbusy = __ballot(role != 0);
+        if (!bbusy) {
+            if (exhausted) break;
+            continue;
+        }
+        if (STATS) {
+            if (role != 0 && !waiting && sub == 0) ps->c[exhausted ? RT_STAT_DRAIN_VISITS : RT_STAT_QUAD_VISITS]++;
+            if (lane == 0) ps->c[exhausted ? RT_STAT_DRAIN_SLOTS : RT_STAT_WAVE_SLOTS] += 16;
+        }
+        const int owner = role == 2 ? vq : bq;
+        int* orec = s_coop + 8 * owner;
+        if (role != 0 && !waiting) {
+            if (orec[2] != 0) {  // the walk is decided (an occluder, or an abort) elsewhere
+                if (role == 2) {
+                    if (sub == 0) atomicSub(&orec[1], 1);
+                    role = 0;
+                } else {
+                    waiting = true;
+                }
+            } else {
+                if (role == 1) q.bot = orec[0];
+                const int res = rtk::quad_visit<true>(S, q, stk, sub, ps);
+                if (res != 0) {
+                    // bit 0: an occluder (the answer), bit 1: a stack overflowed (the exact walk decides)
+                    if (sub == 0 && (res < 0 || q.h.k == 1)) atomicOr(&orec[2], res < 0 ? 2 : 1);
+                    if (role == 2) {
+                        if (sub == 0) atomicSub(&orec[1], 1);
+                        role = 0;
+                    } else {
+                        waiting = true;
+                    }
+                }
+            }
+        }
+        if (role == 1 && waiting && orec[1] == 0) {  // own part and every helper done
+            role = 0;
+            waiting = false;
+            if (sub == 0) {
+                const int f = orec[2];
+                if (f == 2) {  // no occluder found and a part overflowed: the exact walk answers it (k_step(i))
+                    r.d.w = rt_asfloat(target & 7u);
+                    fbl[atomicAdd(fbn, 1)] = r;
+                    atomicAdd(&W.r_park[target >> 3], 1);
+                } else {
+                    rtk::finish_any(W, target, (f & 1) != 0);
+                }
+            }
+        }
+    }
+}
+
 template <bool STATS>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_OCC, 8))) void k_trace(rtk::WaveView W, int par, unsigned long long* stats)
 {
     __shared__ uint32_t s_lds[RT_LDS_WORDS * 256];
     __shared__ int s_pre[rtk::RK_COUNT * RT_QSHARDS + 1];
+#if RT_TRACE_STEAL
+    __shared__ int s_coop[9 * 64];
+#endif
     int32_t* cnt = W.counters;
     if (blockIdx.x == 0) {  // filled by k_step(i) next
         for (int j = threadIdx.x; j < (rtk::RK_COUNT + 1) * RT_QSHARDS; j += blockDim.x)
@@ -687,7 +841,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_OC
     if (closest)
         trace_stream<false, STATS>(W, S, stk, s_pre, c0, total, wg, wn, fbn, fbl, ps);
     else
+#if RT_TRACE_STEAL
+        trace_stream_any_coop<STATS>(W, S, stk, s_pre, a0, total, wg, wn, fbn, fbl, s_coop, ps);
+#else
         trace_stream<true, STATS>(W, S, stk, s_pre, a0, total, wg, wn, fbn, fbl, ps);
+#endif
 #else
     const int sub = (int)(threadIdx.x & 3);
     for (int base = wg * 16; base < total; base += wn * 16) {
