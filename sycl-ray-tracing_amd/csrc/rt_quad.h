@@ -403,6 +403,7 @@ struct QState {
     FastHit h;
     int sp, cur;
     int bot;  // occlusion walks shared with other quads (k_trace drain): entries below bot were taken
+    int calls;  // quad_visit calls so far (k_trace: the heavy-class prediction)
 };
 
 // false: the answer is already known (a NaN ray: no hit), no trip needed.

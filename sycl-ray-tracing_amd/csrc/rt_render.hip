@@ -1,19 +1,22 @@
 // rt_render.hip — gfx950 backend of librt_hip.so: device buffers, the
 // wavefront render kernels and their launches.
 //
-// A render is a loop of iterations over the in-flight path slots (one slot
-// per pixel of the launch):
-//   k_step          resolve last bounce, consume the continuation query,
-//                   shade the new hit (RNG draws, sampling) or end the
-//                   sample / start the next one; appends the emitted rays to
-//                   five per-kind queues and the live slot to the next
-//                   active list (wave-aggregated atomics, no host round trip)
-//   k_trace_closest continuation, light-shadow and BRDF->light queries
-//                   (exact reference traversal, rt_trace.h trace_closest)
-//   k_trace_any     env-shadow and BRDF->env occlusion queries (trace_any)
-// Queue sizes live in device memory; kernels read them and fetch work in
-// 64-ray tickets, so the host only launches and, every few iterations,
-// reads the live-slot count.
+// A render (run_wave) is a loop of iterations over the in-flight path slots
+// (one slot per pixel of the launch), split into up to 3 independent lanes on
+// their own streams:
+//   k_trace  every closest-hit and occlusion query of the iteration, walked
+//            by quads of lanes over the search BVH with octree verification
+//            (rt_quad.h), as a per-wave stream with quad refill; queries it
+//            cannot settle go to the fallback lists
+//   k_step   its first blocks walk the fallbacks (and resume parked walks)
+//            with the exact octree walk (rt_traverse.h); the rest resolve the
+//            last bounce, shade the new hit (RNG draws, sampling) or end the
+//            sample / start the next one, and append the emitted rays to five
+//            per-kind queues (64-way sharded, wave-aggregated atomics)
+//   k_tail   once few paths are left: all of them in one launch, each wave
+//            stepping its own paths and tracing their rays with its quads
+// Queue sizes live in device memory; the host only launches and, every 8
+// iterations, reads the live-slot count.
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -88,8 +91,11 @@ enum {
     C_SHARDED = 64,  // sharded counters from here (qc_at / ac_at)
 };
 #define RT_QSHARDS 64
+#define RT_HSHARDS 8   // heavy-class shards per kind (input shard sh -> heavy shard sh % 8)
 #define RT_CSTRIDE 32  // ints from one sharded counter to the next (one 128-B line each)
-#define C_COUNT (C_SHARDED + (2 * rtk::RK_COUNT + 2) * RT_QSHARDS * RT_CSTRIDE)
+#define C_HEAVY (C_SHARDED + (2 * rtk::RK_COUNT + 2) * RT_QSHARDS * RT_CSTRIDE)
+#define C_COUNT (C_HEAVY + 2 * rtk::RK_COUNT * RT_HSHARDS * RT_CSTRIDE)
+#define C_ZERO (C_SHARDED - 1)  // never written: the count of a padding segment
 __host__ __device__ __forceinline__ int qc_at(int par, int kind, int shard)
 {
     return C_SHARDED + ((par * rtk::RK_COUNT + kind) * RT_QSHARDS + shard) * RT_CSTRIDE;
@@ -97,6 +103,46 @@ __host__ __device__ __forceinline__ int qc_at(int par, int kind, int shard)
 __host__ __device__ __forceinline__ int ac_at(int par, int shard)
 {
     return C_SHARDED + ((2 * rtk::RK_COUNT + par) * RT_QSHARDS + shard) * RT_CSTRIDE;
+}
+__host__ __device__ __forceinline__ int hc_at(int par, int kind, int shard)
+{
+    return C_HEAVY + ((par * rtk::RK_COUNT + kind) * RT_HSHARDS + shard) * RT_CSTRIDE;
+}
+
+// Queue segments in k_trace's stream order. Each role's heavy class comes first, so the
+// walks predicted long (their path's previous query of the kind took >= W.heavy_calls
+// trips) start at the head of every wave's stream instead of setting its drain:
+//   [closest kinds' heavy shards][closest kinds' shards][occlusion kinds' heavy][occlusion kinds']
+// then zero-count padding to a multiple of 64 (shard_prefix).
+#define RT_NCK 3  // closest kinds: CONT, LSH, BL
+#define RT_SEG_CH (RT_NCK * RT_HSHARDS)
+#define RT_SEG_AH (RT_SEG_CH + RT_NCK * RT_QSHARDS)
+#define RT_SEG_A (RT_SEG_AH + (rtk::RK_COUNT - RT_NCK) * RT_HSHARDS)
+#define RT_SEG_END (RT_SEG_A + (rtk::RK_COUNT - RT_NCK) * RT_QSHARDS)
+#define RT_NSEG ((RT_SEG_END + 63) / 64 * 64)
+struct SegId {
+    int kind, shard;
+    bool heavy;
+};
+__host__ __device__ __forceinline__ SegId seg_id(int j)
+{
+    SegId s;
+    if (j < RT_SEG_CH) {
+        s.heavy = true, s.kind = j / RT_HSHARDS, s.shard = j % RT_HSHARDS;
+    } else if (j < RT_SEG_AH) {
+        s.heavy = false, s.kind = (j - RT_SEG_CH) / RT_QSHARDS, s.shard = (j - RT_SEG_CH) % RT_QSHARDS;
+    } else if (j < RT_SEG_A) {
+        s.heavy = true, s.kind = RT_NCK + (j - RT_SEG_AH) / RT_HSHARDS, s.shard = (j - RT_SEG_AH) % RT_HSHARDS;
+    } else {
+        s.heavy = false, s.kind = RT_NCK + (j - RT_SEG_A) / RT_QSHARDS, s.shard = (j - RT_SEG_A) % RT_QSHARDS;
+    }
+    return s;
+}
+__host__ __device__ __forceinline__ int seg_counter(int par, int j)
+{
+    if (j >= RT_SEG_END) return C_ZERO;
+    const SegId s = seg_id(j);
+    return s.heavy ? hc_at(par, s.kind, s.shard) : qc_at(par, s.kind, s.shard);
 }
 
 struct Backend {
@@ -211,6 +257,41 @@ __device__ __forceinline__ void append_emit(const rtk::WaveView& W, int pout, in
     const int cps = ((n_in + 63) / 64 + RT_QSHARDS - 1) / RT_QSHARDS;  // chunks per shard
     const int sh = min(RT_QSHARDS - 1, (base >> 6) / cps);
     const size_t seg = (size_t)sh * W.seg_cap;
+    const unsigned long long lt = (lane_id() == 0) ? 0ull : (~0ull >> (64 - lane_id()));
+    if (W.r_heavy) {  // heavy class on: the rays of a path flagged heavy go to its kind's heavy shard
+        const int hs = sh % RT_HSHARDS;
+        const size_t hseg = ((size_t)RT_QSHARDS + (size_t)hs * (RT_QSHARDS / RT_HSHARDS)) * W.seg_cap;
+        unsigned long long b[2 * rtk::RK_COUNT + 1];
+#pragma unroll
+        for (int k = 0; k < rtk::RK_COUNT; k++) {
+            const bool m = (e.mask >> k) & 1u;
+            b[k] = __ballot(m && !e.heavy);
+            b[rtk::RK_COUNT + k] = __ballot(m && e.heavy);
+        }
+        b[2 * rtk::RK_COUNT] = __ballot(e.active);
+        int r[2 * rtk::RK_COUNT + 1];
+        if (lane_id() == 0) {
+#pragma unroll
+            for (int k = 0; k <= 2 * rtk::RK_COUNT; k++) {
+                const int c = k < rtk::RK_COUNT ? qc_at(pout, k, sh)
+                              : k < 2 * rtk::RK_COUNT ? hc_at(pout, k - rtk::RK_COUNT, hs)
+                                                      : ac_at(pout, sh);
+                r[k] = b[k] ? atomicAdd(W.counters + c, __popcll(b[k])) : 0;
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < rtk::RK_COUNT; k++) {
+            const int kk = e.heavy ? rtk::RK_COUNT + k : k;
+            const int i = __shfl(r[k], 0) + __popcll(b[k] & lt);
+            const int ih = __shfl(r[rtk::RK_COUNT + k], 0) + __popcll(b[rtk::RK_COUNT + k] & lt);
+            if ((e.mask >> k) & 1u) {
+                W.q[k][kk == k ? seg + i : hseg + ih] = e.r[k];
+            }
+        }
+        const int a = __shfl(r[2 * rtk::RK_COUNT], 0) + __popcll(b[2 * rtk::RK_COUNT] & lt);
+        if (e.active) W.act_out[seg + a] = p;
+        return;
+    }
     // the six reservations (five queues, the live list) issued back to back by lane 0
     // and waited for once, then the stores: one atomic round trip, not six in a row
     unsigned long long b[rtk::RK_COUNT + 1];
@@ -225,7 +306,6 @@ __device__ __forceinline__ void append_emit(const rtk::WaveView& W, int pout, in
                                     __popcll(b[k]))
                         : 0;
     }
-    const unsigned long long lt = (lane_id() == 0) ? 0ull : (~0ull >> (64 - lane_id()));
 #pragma unroll
     for (int k = 0; k < rtk::RK_COUNT; k++) {
         const int i = __shfl(r[k], 0) + __popcll(b[k] & lt);
@@ -234,6 +314,7 @@ __device__ __forceinline__ void append_emit(const rtk::WaveView& W, int pout, in
     const int a = __shfl(r[rtk::RK_COUNT], 0) + __popcll(b[rtk::RK_COUNT] & lt);
     if (e.active) W.act_out[seg + a] = p;
 }
+
 
 // Exclusive prefix sums of the sharded counters at cnt[at(j)], j < m (m a
 // multiple of 64), into pre[0..m] (LDS); every thread of the block calls.
@@ -278,6 +359,21 @@ __device__ __forceinline__ int shard_find(const int* pre, int m, int g)
     return lo;
 }
 
+// Queue item of stream position g (segment table pre[0..RT_NSEG], k_trace): the ray and its kind.
+__device__ __forceinline__ rtk::RayRec queue_item_at(const rtk::WaveView& W, const int* pre, int g, int& kind)
+{
+    const int j = shard_find(pre, RT_NSEG, g);
+    const SegId s = seg_id(j);
+    kind = s.kind;
+    // (the queue base by selects: W.q[kind] with a lane-varying kind would be a load)
+    rtk::RayRec* qk = W.q[0];
+#pragma unroll
+    for (int k2 = 1; k2 < rtk::RK_COUNT; k2++) qk = s.kind == k2 ? W.q[k2] : qk;
+    // (heavy shard h: after the kind's RT_QSHARDS segments, RT_QSHARDS / RT_HSHARDS of them each)
+    const int seg0 = s.heavy ? RT_QSHARDS + s.shard * (RT_QSHARDS / RT_HSHARDS) : s.shard;
+    return qk[(size_t)seg0 * W.seg_cap + (g - pre[j])];
+}
+
 // Path init: every slot seeds its RNG and emits its first camera ray (into Q[0], ACT[0]).
 __global__ __launch_bounds__(256) void k_init(rtk::WaveView W)
 {
@@ -286,6 +382,7 @@ __global__ __launch_bounds__(256) void k_init(rtk::WaveView W)
     rtk::Emit e;
     e.mask = 0;
     e.active = false;
+    e.heavy = false;
     if (p < W.n_slots) rtk::path_init(W, p, e);
     append_emit(W, 0, p & ~63, W.n_slots, p, e);
 }
@@ -319,6 +416,12 @@ __global__ __launch_bounds__(256) void k_init(rtk::WaveView W)
 #ifndef RT_TRACE_REFILL
 #define RT_TRACE_REFILL 4       // k_trace: idle quads of a wave that trigger a refill from its query stream (0: static
                                 // 16-query chunks). r02 sweep on cfg2 (RT_VISIT_DESCEND 2): 4 / 8 -> 726 / 723 vs 678 static
+#endif
+#ifndef RT_HEAVY_CALLS
+#define RT_HEAVY_CALLS 6        // heavy class (seg_id): quad_visit calls of a walk that flag its path (0: off).
+                                // cfg2 (r02): off / 3 / 6 / 10 / 16 -> 737 / 744 / 744-748 / 740 / 735 Msamples/s;
+                                // 1-lane k_trace 124.1 -> 117.2 ms, drain slots 838 M -> 737 M
+                                // (a dynamic, per-XCD-ticketed tail of the stream, 10-40 %: 684-691, rejected)
 #endif
 #ifndef RT_TRACE_OCC
 #define RT_TRACE_OCC 6          // k_trace waves per SIMD (8 fits the quad walks in 64 VGPRs but measured
@@ -540,6 +643,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_STEP_OCC
         rtk::Emit e;
         e.mask = 0;
         e.active = false;
+        e.heavy = false;
         int p = -1;
         if (idx < n) {
             const int sh = shard_find(s_pre, RT_QSHARDS, idx);
@@ -571,13 +675,8 @@ __device__ __forceinline__ void trace_stream(const rtk::WaveView& W, const RtSce
                 const int j = cursor + __popcll(bidle & ((1ull << (qd * 4)) - 1ull));  // this quad's stream position
                 const int idx = (wg + (j >> 4) * wn) * 16 + (j & 15);
                 if (idx < total) {
-                    const int g = first + idx;
-                    const int seg = shard_find(s_pre, rtk::RK_COUNT * RT_QSHARDS, g);
-                    const int kind = seg / RT_QSHARDS;
-                    rtk::RayRec* qk = W.q[0];
-#pragma unroll
-                    for (int k2 = 1; k2 < rtk::RK_COUNT; k2++) qk = kind == k2 ? W.q[k2] : qk;
-                    r = qk[(size_t)(seg % RT_QSHARDS) * W.seg_cap + (g - s_pre[seg])];
+                    int kind;
+                    r = queue_item_at(W, s_pre, first + idx, kind);
                     target = (rt_asuint(r.o.w) << 3) | (uint32_t)kind;
                     if (forced_fallback(W, r.o, r.d)) {
                         if (sub == 0) {
@@ -587,6 +686,7 @@ __device__ __forceinline__ void trace_stream(const rtk::WaveView& W, const RtSce
                         }
                     } else if (rtk::qstate_begin<ANY>(q, rtk::v3of(r.o), rtk::v3of(r.d), sub, ps)) {
                         active = true;
+                        q.calls = 0;
                     } else if (sub == 0) {  // (a NaN ray: no hit)
                         if (ANY)
                             rtk::finish_any(W, target, false);
@@ -609,8 +709,11 @@ __device__ __forceinline__ void trace_stream(const rtk::WaveView& W, const RtSce
         }
         if (active) {
             int res = rtk::quad_visit<ANY>(S, q, stk, sub, ps);
+            q.calls++;
             if (res != 0) {
                 active = false;
+                // a long walk: the path's next rays go to the heavy class (head of the next streams)
+                if (W.r_heavy && sub == 0 && q.calls >= W.heavy_calls) W.r_heavy[target >> 3] = 1;
                 float t = 0.0f;
                 int k = 0;
                 if (res > 0 && !ANY && !rtk::quad_closest_answer(S, q, sub, t, k, ps)) res = -1;
@@ -662,13 +765,8 @@ __device__ __forceinline__ void trace_stream_any_coop(const rtk::WaveView& W, co
                 const int j = cursor + __popcll(bidle & ((1ull << (qd * 4)) - 1ull));
                 const int idx = (wg + (j >> 4) * wn) * 16 + (j & 15);
                 if (idx < total) {
-                    const int g = first + idx;
-                    const int seg = shard_find(s_pre, rtk::RK_COUNT * RT_QSHARDS, g);
-                    const int kind = seg / RT_QSHARDS;
-                    rtk::RayRec* qk = W.q[0];
-#pragma unroll
-                    for (int k2 = 1; k2 < rtk::RK_COUNT; k2++) qk = kind == k2 ? W.q[k2] : qk;
-                    r = qk[(size_t)(seg % RT_QSHARDS) * W.seg_cap + (g - s_pre[seg])];
+                    int kind;
+                    r = queue_item_at(W, s_pre, first + idx, kind);
                     target = (rt_asuint(r.o.w) << 3) | (uint32_t)kind;
                     if (forced_fallback(W, r.o, r.d)) {
                         if (sub == 0) {
@@ -783,7 +881,7 @@ template <bool STATS>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_OCC, 8))) void k_trace(rtk::WaveView W, int par, unsigned long long* stats)
 {
     __shared__ uint32_t s_lds[RT_LDS_WORDS * 256];
-    __shared__ int s_pre[rtk::RK_COUNT * RT_QSHARDS + 1];
+    __shared__ int s_pre[RT_NSEG + 1];
 #if RT_TRACE_STEAL
     __shared__ int s_coop[9 * 64];
 #endif
@@ -792,6 +890,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_OC
         for (int j = threadIdx.x; j < (rtk::RK_COUNT + 1) * RT_QSHARDS; j += blockDim.x)
             cnt[j < rtk::RK_COUNT * RT_QSHARDS ? qc_at(par ^ 1, j / RT_QSHARDS, j % RT_QSHARDS)
                                                 : ac_at(par ^ 1, j - rtk::RK_COUNT * RT_QSHARDS)] = 0;
+        for (int j = threadIdx.x; j < rtk::RK_COUNT * RT_HSHARDS; j += blockDim.x)
+            cnt[hc_at(par ^ 1, j / RT_HSHARDS, j % RT_HSHARDS)] = 0;
         if (threadIdx.x == 0) {
             cnt[C_PARKC0 + par] = cnt[C_PARKA0 + par] = 0;
             cnt[C_TK_EXACT_C] = cnt[C_TK_EXACT_A] = 0;
@@ -814,13 +914,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_OC
     S.bvh4_top = rtk::top_nodes_stage(S);
     // fast roles: a quad of lanes per query (rt_quad.h), 16 queries per wave
     rtk::QuadStack<RT_QSTACK, 64> stk{s_lds + (threadIdx.x >> 2), (float*)s_lds + RT_QSTACK * 64 + (threadIdx.x >> 2)};
-    // queue segments (kind-major, then shard): prefix table in LDS
-    shard_prefix(cnt, rtk::RK_COUNT * RT_QSHARDS,
-                 [&](int j) { return qc_at(par, j / RT_QSHARDS, j % RT_QSHARDS); }, s_pre);
-    const int last_kind = W.any_rays ? rtk::RK_BL : rtk::RK_BENV;
-    const int c0 = s_pre[rtk::RK_CONT * RT_QSHARDS], a0 = s_pre[rtk::RK_ESH * RT_QSHARDS];
-    const int nc = s_pre[(last_kind + 1) * RT_QSHARDS] - c0;
-    const int na = W.any_rays ? s_pre[(rtk::RK_BENV + 1) * RT_QSHARDS] - a0 : 0;
+    // queue segments in stream order (seg_id: each role's heavy class first): prefix table in LDS
+    shard_prefix(cnt, RT_NSEG, [&](int j) { return seg_counter(par, j); }, s_pre);
+    // without occlusion walks (analytic spheres) every kind is a closest-hit query
+    const int c0 = 0, a0 = s_pre[RT_SEG_AH];
+    const int nc = (W.any_rays ? a0 : s_pre[RT_SEG_END]) - c0;
+    const int na = W.any_rays ? s_pre[RT_SEG_END] - a0 : 0;
     if (STATS && W.iterq && b == 0 && threadIdx.x == 0 && W.iter < RT_MAX_TIMED_ITERS) W.iterq[2 * W.iter] = nc + na;
     const int fb0 = 0, nbf = (int)gridDim.x;
     const int nbc = split_blocks(nbf, nc, na);
@@ -863,14 +962,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_OC
         const unsigned long long v0 = STATS ? st.c[RT_STAT_VOL] + st.c[RT_STAT_ANY_VOL] : 0;
         if (idx < total) {
             // queue item: segment (kind, shard) of global index g
-            const int g = (closest ? c0 : a0) + idx;
-            const int seg = shard_find(s_pre, rtk::RK_COUNT * RT_QSHARDS, g);
-            const int kind = seg / RT_QSHARDS;
-            // (the queue base by selects: W.q[kind] with a lane-varying kind would be a load)
-            rtk::RayRec* qk = W.q[0];
-#pragma unroll
-            for (int k2 = 1; k2 < rtk::RK_COUNT; k2++) qk = kind == k2 ? W.q[k2] : qk;
-            r = qk[(size_t)(seg % RT_QSHARDS) * W.seg_cap + (g - s_pre[seg])];
+            int kind;
+            r = queue_item_at(W, s_pre, (closest ? c0 : a0) + idx, kind);
             target = (rt_asuint(r.o.w) << 3) | (uint32_t)kind;
             if (forced_fallback(W, r.o, r.d)) {
                 fail = sub == 0;
@@ -1015,6 +1108,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TAIL_OCC
         rtk::Emit e;
         e.mask = 0;
         e.active = false;
+        e.heavy = false;
         const long long t0 = probe ? wall_clock64() : 0;
         if (my >= 0) {
             rtk::path_step(W, my, e, ps);
@@ -1580,6 +1674,8 @@ int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounces, cons
     WaveLane L[RT_MAX_LANES];
     int force_fb = 0;
     if (const char* e = getenv("RT_FORCE_FALLBACK")) force_fb = std::max(0, atoi(e));
+    int heavy_calls = RT_HEAVY_CALLS;
+    if (const char* e = getenv("RT_HEAVY")) heavy_calls = std::max(0, atoi(e));
     int tail_p = 5;  // (5 paths: 15 queries, one pass of the wave's 16 quads; sweep 2-6 within 1 %)
     if (const char* e = getenv("RT_TAIL_PATHS")) tail_p = std::min(RT_TAIL_MAXP, std::max(0, atoi(e)));
     const int tail_blocks = dev_cus * RT_TAIL_OCC;  // one grid-fill of k_tail
@@ -1616,6 +1712,7 @@ int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounces, cons
         La.tev = b->tev[l];
         rtk::WaveView& W = La.W;
         W.park_cap = 1 << 16;
+        W.heavy_calls = heavy_calls;
         W.shards = RT_QSHARDS;
         W.seg_cap = 64 * (((La.n + 63) / 64 + RT_QSHARDS - 1) / RT_QSHARDS);  // (append_emit: chunks per shard)
         W.spill_lanes = dev_cus * 4 * threads;  // exact walks: up to dev_cus * 2 blocks per role

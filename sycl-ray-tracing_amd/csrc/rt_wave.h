@@ -79,10 +79,9 @@ struct WaveView {
     float4_* p_fin;         // fin.rgb
     // pending bounce (shade -> resolve)
     float4_* q_light;       // light candidate rgb, dist
-    float4_* q_bl;          // BRDF->light sample brdf rgb, pdf
+    float4_* q_bl;          // BRDF->light sample brdf * cos(n, dir) rgb, pdf
     float4_* q_sdir;        // BRDF->light dir xyz
     float4_* q_blo;         // BRDF->light origin xyz (sphere hit normals)
-    float4_* q_hn;          // hit normal xyz
     float4_* q_env;         // env candidate rgb
     float4_* q_benv;        // BRDF->env candidate rgb
     float4_* q_em;          // emission rgb (bounce 0)
@@ -96,7 +95,9 @@ struct WaveView {
     uint8_t* r_esh;
     uint8_t* r_benv;
     // queues
-    RayRec* q[RK_COUNT];    // [n_slots] each
+    RayRec* q[RK_COUNT];    // [shards * seg_cap] each, then (heavy class on) as many of its heavy class
+    uint8_t* r_heavy;       // [n_slots] (heavy class on) a query of the slot took >= heavy_calls quad trips
+    int heavy_calls;        // k_trace's heavy threshold (0: heavy class off; set before wave_carve)
     int32_t* counters;      // queue sizes, tickets, live counts (rt_render.hip C_*)
     int32_t* r_park;        // [n_slots] queries of the slot parked (the step skips the slot while > 0)
     RayRec* fb_c[2];        // [5 n_slots] closest-hit queries left to the exact walk (d.w = kind), by parity
@@ -148,7 +149,6 @@ inline size_t wave_carve(char* base, size_t n, WaveView& W)  // uses W.park_cap,
     W.q_bl = (float4_*)take(n * 16);
     W.q_sdir = (float4_*)take(n * 16);
     W.q_blo = (float4_*)take(n * 16);
-    W.q_hn = (float4_*)take(n * 16);
     W.q_env = (float4_*)take(n * 16);
     W.q_benv = (float4_*)take(n * 16);
     W.q_em = (float4_*)take(n * 16);
@@ -161,7 +161,8 @@ inline size_t wave_carve(char* base, size_t n, WaveView& W)  // uses W.park_cap,
     W.r_esh = (uint8_t*)take(n);
     W.r_benv = (uint8_t*)take(n);
     const size_t qn = (size_t)W.shards * W.seg_cap;  // >= n
-    for (int k = 0; k < RK_COUNT; k++) W.q[k] = (RayRec*)take(qn * sizeof(RayRec));
+    for (int k = 0; k < RK_COUNT; k++) W.q[k] = (RayRec*)take((W.heavy_calls > 0 ? 2 : 1) * qn * sizeof(RayRec));
+    W.r_heavy = W.heavy_calls > 0 ? (uint8_t*)take(n) : nullptr;
     W.act_in = (const int32_t*)take(qn * 4);
     W.act_out = (int32_t*)take(qn * 4);
     W.r_park = (int32_t*)take(n * 4);
@@ -189,6 +190,7 @@ struct Emit {
     RayRec r[RK_COUNT];
     uint32_t mask;  // bit k: a ray of kind k
     bool active;    // the path stays in flight
+    bool heavy;     // the rays go to the heavy class (WaveView::qh)
 };
 
 RT_HD void emit(Emit& e, int kind, int slot, V3 o, V3 d)
@@ -250,13 +252,14 @@ RT_HD void load_path(const WaveView& W, int p, PathReg& P)
     P.fin = colof(e);
 }
 
-RT_HD void store_path(const WaveView& W, int p, const PathReg& P)
+// fin changes only when a sample ends: the other steps leave its record alone
+RT_HD void store_path(const WaveView& W, int p, const PathReg& P, bool fin_changed)
 {
     W.p_ro[p] = f4(P.ro, rt_asfloat(P.rng.a));
     W.p_rd[p] = f4(P.rd, rt_asfloat(P.flags | ((uint32_t)P.bounce << 8)));
     W.p_thr[p] = f4(P.thr, rt_asfloat((uint32_t)P.sample));
     W.p_sc[p] = f4(P.sc, 0.0f);
-    W.p_fin[p] = f4(P.fin, 0.0f);
+    if (fin_changed) W.p_fin[p] = f4(P.fin, 0.0f);
 }
 
 // Camera ray of the next sample (render_kernel.cpp:88-92, get_camera_ray
@@ -324,9 +327,10 @@ RT_HD void path_init(const WaveView& W, int p, Emit& e)
     P.fin = col(0.0f);
     P.sample = 0;
     e.mask = 0;
+    e.heavy = false;
     e.active = start_sample(W, p, P, e);
     if (!e.active) finish_pixel(W, p, P);
-    store_path(W, p, P);
+    store_path(W, p, P, true);
 }
 
 // Hit record of a closest-hit query (HitInfo fields the integrator reads).
@@ -413,7 +417,9 @@ RT_HD void shade(const WaveView& W, int p, PathReg& P, const Hit& h, Emit& e, St
         float dpdf;
         Col brdf = ct_sample(m, neg(rd), h.n, sdir, dpdf, P.rng);
         if (!(brdf.r == 0.0f && brdf.g == 0.0f && brdf.b == 0.0f) && W.bl_rays) {
-            W.q_bl[p] = f4(brdf, dpdf);
+            // brdf * dot(n, sdir): the first product of resolve's bmis (:700), done here so the
+            // hit normal need not travel
+            W.q_bl[p] = f4(cscale(brdf, dot(h.n, sdir)), dpdf);
             const V3 blo = add(h.p, mul(1.0e-5f, h.n));
             W.q_sdir[p] = f4(sdir, 0.0f);
             W.q_blo[p] = f4(blo, 0.0f);
@@ -472,7 +478,6 @@ RT_HD void shade(const WaveView& W, int p, PathReg& P, const Hit& h, Emit& e, St
         fl |= PF_EMIT0;
         W.q_em[p] = f4(m.emission, 0.0f);
     }
-    W.q_hn[p] = f4(h.n, 0.0f);
     W.q_thr[p] = f4(P.thr, 0.0f);
     if ((brdf.r == 0.0f && brdf.g == 0.0f && brdf.b == 0.0f) || bpdf < 1.0e-8f || rt_isinf(bpdf)) {
         fl |= PF_END;  // `break` after this bounce's light is added
@@ -500,8 +505,10 @@ RT_HD void resolve(const WaveView& W, int p, PathReg& P, Stats* st)
     const RtSceneView& S = W.S;
     const uint32_t fl = P.flags;
     // the records every resolve reads, loaded together up front (one memory round trip)
-    const float4_ q_thr = W.q_thr[p], q_env = W.q_env[p], q_benv = W.q_benv[p];
-    const uint8_t r_esh = W.r_esh[p], r_benv = W.r_benv[p];
+    const float4_ z = float4_{0.0f, 0.0f, 0.0f, 0.0f};
+    const float4_ q_thr = W.q_thr[p];
+    const float4_ q_env = (fl & PF_ESH) ? W.q_env[p] : z, q_benv = (fl & PF_BENV) ? W.q_benv[p] : z;
+    const uint8_t r_esh = (fl & PF_ESH) ? W.r_esh[p] : 1, r_benv = (fl & PF_BENV) ? W.r_benv[p] : 1;
     Col light = col(0.0f);
     if (fl & PF_LSH) {
         const float4_ q = W.q_light[p];
@@ -516,7 +523,6 @@ RT_HD void resolve(const WaveView& W, int p, PathReg& P, Stats* st)
             const int k = W.r_bl_k[p];
             const float4_ qb = W.q_bl[p];
             const V3 sdir = v3of(W.q_sdir[p]);
-            const V3 hn = v3of(W.q_hn[p]);
             Hit nh;
             hit_from(S, v3of(W.q_blo[p]), sdir, t, k, nh);
             float ca = rt_max(dot(nh.n, neg(sdir)), 0.0f);
@@ -532,8 +538,7 @@ RT_HD void resolve(const WaveView& W, int p, PathReg& P, Stats* st)
                     float la = k < 0 ? 0.0f : length(cross(ld3(S.tri4[3 * k + 1]), ld3(S.tri4[3 * k + 2]))) / 2;
                     float lp = d2 / (la * ca);
                     float mis = power_heuristic(qb.w, lp);
-                    float cosine = dot(hn, sdir);
-                    bmis = cdiv(cscale(cmul(cscale(colof(qb), cosine), e), mis), qb.w);
+                    bmis = cdiv(cscale(cmul(colof(qb), e), mis), qb.w);  // (qb.rgb = brdf * cosine, shade)
                 }
             }
         }
@@ -554,13 +559,19 @@ RT_HD void path_step(const WaveView& W, int p, Emit& e, Stats* st)
 {
     e.mask = 0;
     e.active = true;
+    e.heavy = false;
     // the slot's state, wait count and continuation result in one round trip
     const int park = W.r_park[p];
+    const int heavy = W.r_heavy ? W.r_heavy[p] : 0;
     PathReg P;
     load_path(W, p, P);
     const float cont_t = W.r_cont_t[p];
     const int cont_k = W.r_cont_k[p];
     if (park != 0) return;  // a query of this path is parked: wait
+    if (heavy) {  // its last walk was long: this step's rays head the next streams
+        e.heavy = true;
+        W.r_heavy[p] = 0;
+    }
     if (P.flags & PF_AUX) resolve(W, p, P, st);
     bool end = (P.flags & PF_END) != 0;
     if (P.flags & PF_CONT) {
@@ -568,7 +579,7 @@ RT_HD void path_step(const WaveView& W, int p, Emit& e, Stats* st)
         Hit h;
         if (hit_from(W.S, P.ro, P.rd, t, cont_k, h)) {
             shade(W, p, P, h, e, st);
-            store_path(W, p, P);
+            store_path(W, p, P, false);
             return;
         }
         // MISSED (:143-160): the next loop iteration adds the sky only when
@@ -585,7 +596,7 @@ RT_HD void path_step(const WaveView& W, int p, Emit& e, Stats* st)
         }
         if (!e.active) finish_pixel(W, p, P);
     }
-    store_path(W, p, P);
+    store_path(W, p, P, end);
 }
 
 // --------------------------------------------------------------- queries
