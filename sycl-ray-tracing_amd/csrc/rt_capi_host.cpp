@@ -45,6 +45,7 @@ RtSceneView rt_host_view(const rt_context* c)
     v.cdf_fence = c->cdf_fence.empty() ? nullptr : c->cdf_fence.data();
     v.cdf_coarse = c->cdf_coarse.data();
     v.cdf_cw = c->cdf_cw;
+    v.cdf_total = c->cdf.empty() ? 0.0f : c->cdf.back();
     v.n_emissive = (int)c->emissive.size();
     v.n_spheres = (int)(c->spheres.size() / 2);
     v.ew = c->ew;

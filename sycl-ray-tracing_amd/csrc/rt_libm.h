@@ -390,6 +390,45 @@ RT_HD float cosf_(float y)
     return invalidf();
 }
 
+// sinf_ and cosf_ of one argument from one reduction: the same arithmetic as the two
+// functions above (both polynomials are evaluated once, each result picks its own by n & 1).
+RT_HD void sincosf_(float y, float& so, float& co)
+{
+    const uint32_t iy = rt_asuint(y);
+    const uint32_t abstop = (iy >> 20) & 0x7ff;
+    const double x = (double)y;
+    if (abstop < 0x3f4) {
+        if (abstop < 0x398) {
+            so = y;
+            co = 1.0f;
+            return;
+        }
+        const double x2 = x * x;
+        so = sinf_poly_sin(x, x2, 0);
+        co = sinf_poly_cos(x2, 0);
+        return;
+    }
+    if (abstop < 0x7f8) {
+        int n, nt;
+        double xr;
+        if (abstop < 0x42f) {
+            xr = reduce_fast(x, &n);
+            nt = n;
+        } else {
+            xr = reduce_large(iy, &n);
+            nt = n + (int)(iy >> 31);
+        }
+        const double s = sc_sign(nt);
+        const int tab = (nt & 2) ? 1 : 0;
+        const double x2 = xr * xr;
+        const float ps = sinf_poly_sin(xr * s, x2, tab), pc = sinf_poly_cos(x2, tab);
+        so = (n & 1) == 0 ? ps : pc;
+        co = (n & 1) == 0 ? pc : ps;
+        return;
+    }
+    so = co = invalidf();
+}
+
 // --------------------------------------------------------------------- acosf
 // e_acosf.c (fdlibm, float arithmetic, no contraction).
 RT_HD float acosf_poly_r(float z)
@@ -607,6 +646,7 @@ RT_HD float rt_expf(float x) { return rtlibm::expf_(x); }
 RT_HD float rt_powf(float x, float y) { return rtlibm::powf_(x, y); }
 RT_HD float rt_sinf(float x) { return rtlibm::sinf_(x); }
 RT_HD float rt_cosf(float x) { return rtlibm::cosf_(x); }
+RT_HD void rt_sincosf(float x, float& s, float& c) { rtlibm::sincosf_(x, s, c); }
 RT_HD float rt_acosf(float x) { return rtlibm::acosf_(x); }
 RT_HD float rt_asinf(float x) { return rtlibm::asinf_(x); }
 RT_HD float rt_atan2f(float y, float x) { return rtlibm::atan2f_(y, x); }

@@ -1534,6 +1534,7 @@ int upload_one(rt_context* c, Backend* b, const std::vector<int32_t>& matk, bool
     v.cdf_coarse = (const float*)b->cdf_coarse.p;
     v.cdf_fence = c->cdf_fence.empty() ? nullptr : (const float*)b->cdf_fence.p;
     v.cdf_cw = c->cdf_cw;
+    v.cdf_total = c->cdf.empty() ? 0.0f : c->cdf.back();
     v.n_emissive = (int)c->emissive.size();
     v.n_spheres = (int)(c->spheres.size() / 2);
     v.ew = c->ew;

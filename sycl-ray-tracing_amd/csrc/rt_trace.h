@@ -790,8 +790,10 @@ RT_HD Col ct_sample(const Mat& m, V3 V, V3 N, V3& out_dir, float& pdf, Rng& rng)
     float r2 = rng.next();
     float phi = 2.0f * RT_PI_F * r1;
     float theta = rt_acosf((1.0f - r2) / (r2 * (alpha * alpha - 1.0f) + 1.0f));
-    float sin_theta = rt_sinf(theta);
-    V3 local = v3(rt_cosf(phi) * sin_theta, rt_sinf(phi) * sin_theta, rt_cosf(theta));
+    float sin_theta, cos_theta, sin_phi, cos_phi;
+    rt_sincosf(theta, sin_theta, cos_theta);
+    rt_sincosf(phi, sin_phi, cos_phi);
+    V3 local = v3(cos_phi * sin_theta, sin_phi * sin_theta, cos_theta);
     V3 mn = rotate_around_normal(N, local);
     if (dot(mn, N) < 0.0f) return col(0.0f);
     V3 L = normalize(sub(mul(2.0f * dot(mn, V), mn), V));
@@ -840,24 +842,24 @@ RT_HD Col env_from_dir(const RtSceneView& S, V3 d, Stats* st)  // :520-530
 // every predicate true and returns m, as the loop does. The count is read
 // off three levels of 16 fences, one 64-B load each: block ends at 256 (t[0..16)),
 // block ends at 16 (t[16..272)), then the 16 entries themselves.
+// One level of fence_count: the 16 entries of block b at lv + c / b (one 64-B load).
+RT_HD int fence_level(const float* lv, int c, int b, int m, float value)
+{
+    const float4_* p = (const float4_*)(lv + c / b);
+    const float4_ q0 = p[0], q1 = p[1], q2 = p[2], q3 = p[3];
+    const float k[16] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w,
+                         q2.x, q2.y, q2.z, q2.w, q3.x, q3.y, q3.z, q3.w};
+    int n = 0;
+#pragma unroll
+    for (int j = 0; j < 16; j++) n += (c + b * (j + 1) - 1 < m && !(value < k[j])) ? 1 : 0;
+    return c + n * b;
+}
+
 RT_HD int fence_count(const float* a, const float* t, int m, float value)
 {
-    int c = 0;
-    const float* lv[3] = {t, t + 16, a};
-    const int blk[3] = {256, 16, 1};
-#pragma unroll
-    for (int L = 0; L < 3; L++) {
-        const int b = blk[L];
-        const float4_* p = (const float4_*)(lv[L] + c / b);
-        const float4_ q0 = p[0], q1 = p[1], q2 = p[2], q3 = p[3];
-        const float k[16] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w,
-                             q2.x, q2.y, q2.z, q2.w, q3.x, q3.y, q3.z, q3.w};
-        int n = 0;
-#pragma unroll
-        for (int j = 0; j < 16; j++) n += (c + b * (j + 1) - 1 < m && !(value < k[j])) ? 1 : 0;
-        c += n * b;
-    }
-    return c;
+    int c = fence_level(t, 0, 256, m, value);
+    c = fence_level(t + 16, c, 16, m, value);
+    return fence_level(a, c, 1, m, value);
 }
 
 RT_HD void cdf_search(const RtSceneView& S, float value, int& x, int& y, Stats* st)  // :532-567

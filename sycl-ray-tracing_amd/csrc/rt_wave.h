@@ -334,6 +334,28 @@ RT_HD void path_init(const WaveView& W, int p, Emit& e)
 }
 
 // Hit record of a closest-hit query (HitInfo fields the integrator reads).
+// As hit_from, the triangle's records r0..r2 (tri4[3k..3k+2]) already loaded by the caller.
+RT_HD bool hit_from_rec(const RtSceneView& S, V3 o, V3 d, float t, int k, const float4_& r0, const float4_& r1,
+                        const float4_& r2, Hit& h)
+{
+    h.t = t;
+    h.k = k;
+    h.prim = -1;
+    h.mi = -1;
+    if (k >= 0) {  // triangle (triangle.h:46-56)
+        h.p = add(o, mul(t, d));
+        h.n = normalize(cross(ld3(r1), ld3(r2)));
+        h.prim = (int)rt_asuint(r0.w);
+        if (S.tri_mat) h.mi = (int)rt_asuint(r1.w);
+    } else if (k <= -2) {  // sphere (sphere.h:46-48)
+        const float4_ s0 = S.spheres[2 * (-2 - k)];
+        h.p = add(o, mul(t, d));
+        h.n = normalize(sub(h.p, ld3(s0)));
+        h.prim = (int)rt_asuint(S.spheres[2 * (-2 - k) + 1].x);
+    }
+    return t > 0.0f;
+}
+
 RT_HD bool hit_from(const RtSceneView& S, V3 o, V3 d, float t, int k, Hit& h)
 {
     h.t = t;
@@ -429,14 +451,16 @@ RT_HD void shade(const WaveView& W, int p, PathReg& P, const Hit& h, Emit& e, St
     }
     // ---- sample_environment_map (:569-631)
     {
-        const float total = S.cdf[S.ew * S.eh - 1];
+        const float total = S.cdf_total;
         int x, y;
         cdf_search(S, P.rng.next() * total, x, y, st);
         float u = (float)x / (float)S.ew, v = (float)y / (float)S.eh;
         float phi = (float)((double)(u * 2.0f) * 3.14159265358979323846);
         float theta = (float)((double)v * 3.14159265358979323846);
-        float st_ = rt_sinf(theta), ct_ = rt_cosf(theta);
-        V3 dir = v3(-st_ * rt_cosf(phi), -ct_, -st_ * rt_sinf(phi));
+        float st_, ct_, sp_, cp_;
+        rt_sincosf(theta, st_, ct_);
+        rt_sincosf(phi, sp_, cp_);
+        V3 dir = v3(-st_ * cp_, -ct_, -st_ * sp_);
         float cosine = dot(h.n, dir);
         if (cosine > 0.0f) {
             // the texel and its f64-evaluated luminance in one record (env.w = env_lum, rt_set_env)
@@ -461,7 +485,7 @@ RT_HD void shade(const WaveView& W, int p, PathReg& P, const Hit& h, Emit& e, St
             Col sky = env_from_dir(S, bdir, st);
             float th = rt_acosf(bdir.z);
             float sth = rt_sinf(th);
-            float epdf = (0.3086f * sky.r + 0.6094f * sky.g + 0.0820f * sky.b) / S.cdf[S.ew * S.eh - 1];
+            float epdf = (0.3086f * sky.r + 0.6094f * sky.g + 0.0820f * sky.b) / S.cdf_total;
             epdf *= (float)(S.ew * S.eh);
             epdf = (float)((double)epdf / (2.0 * 3.14159265358979323846 * 3.14159265358979323846 * (double)sth));
             float mis = power_heuristic(bsp, epdf);
@@ -500,25 +524,42 @@ RT_HD void shade(const WaveView& W, int p, PathReg& P, const Hit& h, Emit& e, St
 // sc += (light + bmis + brdf_sample + env_sample) * thr with the
 // reference's association: lr = light + bmis, er = brdf_sample + env_sample,
 // sc = sc + (lr + er) * thr (render_kernel.cpp:113-128).
-RT_HD void resolve(const WaveView& W, int p, PathReg& P, Stats* st)
+// The records a resolve reads first, loaded by path_step together with the hit's
+// triangle (one memory round trip): the pending bounce's candidates and their query results.
+struct ResolveRec {
+    float4_ thr, env, benv, light;
+    float lsh_t, bl_t;
+    uint8_t esh, benv_r;
+};
+RT_HD void resolve_load(const WaveView& W, int p, uint32_t fl, ResolveRec& R)
+{
+    const float4_ z = float4_{0.0f, 0.0f, 0.0f, 0.0f};
+    R.thr = W.q_thr[p];
+    R.env = (fl & PF_ESH) ? W.q_env[p] : z;
+    R.benv = (fl & PF_BENV) ? W.q_benv[p] : z;
+    R.esh = (fl & PF_ESH) ? W.r_esh[p] : 1;
+    R.benv_r = (fl & PF_BENV) ? W.r_benv[p] : 1;
+    R.light = (fl & PF_LSH) ? W.q_light[p] : z;
+    R.lsh_t = (fl & PF_LSH) ? W.r_lsh_t[p] : 0.0f;
+    R.bl_t = (fl & PF_BL) ? W.r_bl_t[p] : 0.0f;
+}
+
+RT_HD void resolve(const WaveView& W, int p, PathReg& P, const ResolveRec& R, Stats* st)
 {
     const RtSceneView& S = W.S;
     const uint32_t fl = P.flags;
-    // the records every resolve reads, loaded together up front (one memory round trip)
-    const float4_ z = float4_{0.0f, 0.0f, 0.0f, 0.0f};
-    const float4_ q_thr = W.q_thr[p];
-    const float4_ q_env = (fl & PF_ESH) ? W.q_env[p] : z, q_benv = (fl & PF_BENV) ? W.q_benv[p] : z;
-    const uint8_t r_esh = (fl & PF_ESH) ? W.r_esh[p] : 1, r_benv = (fl & PF_BENV) ? W.r_benv[p] : 1;
+    const float4_ q_thr = R.thr, q_env = R.env, q_benv = R.benv;
+    const uint8_t r_esh = R.esh, r_benv = R.benv_r;
     Col light = col(0.0f);
     if (fl & PF_LSH) {
-        const float4_ q = W.q_light[p];
-        const float t = W.r_lsh_t[p];
+        const float4_ q = R.light;
+        const float t = R.lsh_t;
         const bool in_shadow = t > 0.0f && t + 1.0e-4f < q.w;
         if (!in_shadow) light = colof(q);
     }
     Col bmis = col(0.0f);
     if (fl & PF_BL) {
-        const float t = W.r_bl_t[p];
+        const float t = R.bl_t;
         if (t > 0.0f) {
             const int k = W.r_bl_k[p];
             const float4_ qb = W.q_bl[p];
@@ -572,12 +613,22 @@ RT_HD void path_step(const WaveView& W, int p, Emit& e, Stats* st)
         e.heavy = true;
         W.r_heavy[p] = 0;
     }
-    if (P.flags & PF_AUX) resolve(W, p, P, st);
+    // what depends only on the state, loaded together: the bounce to resolve and the hit's triangle
+    const uint32_t fl0 = P.flags;
+    ResolveRec R;
+    if (fl0 & PF_AUX) resolve_load(W, p, fl0, R);
+    float4_ tr0 = float4_{0.0f, 0.0f, 0.0f, 0.0f}, tr1 = tr0, tr2 = tr0;
+    if ((fl0 & PF_CONT) && cont_t > 0.0f && cont_k >= 0) {
+        tr0 = W.S.tri4[3 * cont_k];
+        tr1 = W.S.tri4[3 * cont_k + 1];
+        tr2 = W.S.tri4[3 * cont_k + 2];
+    }
+    if (fl0 & PF_AUX) resolve(W, p, P, R, st);
     bool end = (P.flags & PF_END) != 0;
     if (P.flags & PF_CONT) {
         const float t = cont_t;
         Hit h;
-        if (hit_from(W.S, P.ro, P.rd, t, cont_k, h)) {
+        if (hit_from_rec(W.S, P.ro, P.rd, t, cont_k, tr0, tr1, tr2, h)) {
             shade(W, p, P, h, e, st);
             store_path(W, p, P, false);
             return;

@@ -82,6 +82,12 @@ int main(int argc, char** argv)
     if (want("expf")) bad += check_unary("expf", stride, [](float x) { return expf(x); }, rt_expf);
     if (want("sinf")) bad += check_unary("sinf", stride, [](float x) { return sinf(x); }, rt_sinf);
     if (want("cosf")) bad += check_unary("cosf", stride, [](float x) { return cosf(x); }, rt_cosf);
+    if (want("sincosf")) {  // both results of the shared-reduction form, against glibc sinf / cosf
+        bad += check_unary("sincos.s", stride, [](float x) { return sinf(x); },
+                           [](float x) { float s, c; rt_sincosf(x, s, c); return s; });
+        bad += check_unary("sincos.c", stride, [](float x) { return cosf(x); },
+                           [](float x) { float s, c; rt_sincosf(x, s, c); return c; });
+    }
     if (want("acosf")) bad += check_unary("acosf", stride, [](float x) { return acosf(x); }, rt_acosf);
     if (want("asinf")) bad += check_unary("asinf", stride, [](float x) { return asinf(x); }, rt_asinf);
     if (want("powf5"))
