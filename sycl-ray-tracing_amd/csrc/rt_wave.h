@@ -433,12 +433,16 @@ RT_HD void shade(const WaveView& W, int p, PathReg& P, const Hit& h, Emit& e, St
             }
         }
     }
-    // ---- sample_lights, BRDF half (:681-711)
-    {
+    // ---- sample_lights, BRDF half (:681-711). With no emissive material (bl_rays 0) the
+    // sample can never contribute: only its two RNG draws are kept.
+    if (!W.bl_rays) {
+        P.rng.next();
+        P.rng.next();
+    } else {
         V3 sdir = v3(0.0f, 0.0f, 0.0f);
         float dpdf;
         Col brdf = ct_sample(m, neg(rd), h.n, sdir, dpdf, P.rng);
-        if (!(brdf.r == 0.0f && brdf.g == 0.0f && brdf.b == 0.0f) && W.bl_rays) {
+        if (!(brdf.r == 0.0f && brdf.g == 0.0f && brdf.b == 0.0f)) {
             // brdf * dot(n, sdir): the first product of resolve's bmis (:700), done here so the
             // hit normal need not travel
             W.q_bl[p] = f4(cscale(brdf, dot(h.n, sdir)), dpdf);
