@@ -65,6 +65,7 @@ static int run_wave_host(rt_context* c, int w, int h, int spp, int bounces, cons
     W.H = h;
     W.spp = spp;
     W.bounces = bounces;
+    rtk::set_view_consts(W);
     W.n_slots = n;
     W.bl_rays = rt_scene_has_emissive_prim(c) ? 1 : 0;
     W.any_rays = W.S.n_spheres == 0 ? 1 : 0;
@@ -230,6 +231,8 @@ static int run_wave_host(rt_context* c, int w, int h, int spp, int bounces, cons
             }
         }
     }
+#pragma omp parallel for schedule(static)
+    for (int p = 0; p < n; p++) rtk::tonemap_pixel(W, p);
     merge_stats(c, st);
     return RT_OK;
 }

@@ -387,6 +387,14 @@ __global__ __launch_bounds__(256) void k_init(rtk::WaveView W)
     append_emit(W, 0, p & ~63, W.n_slots, p, e);
 }
 
+// After a lane's last step: the tone-map of every pixel of the lane (rt_wave.h tonemap_pixel).
+__global__ __launch_bounds__(256) void k_tonemap(rtk::WaveView W)
+{
+    rtlibm::lds_tables_init();
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p < W.n_slots) rtk::tonemap_pixel(W, p);
+}
+
 // ------------------------------------------------------------- query kernel
 // Every closest-hit and occlusion query of the iteration, plus the exact
 // octree walks of the queries the previous iteration could not settle, in
@@ -1728,6 +1736,7 @@ int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounces, cons
         W.H = h;
         W.spp = spp;
         W.bounces = bounces;
+        rtk::set_view_consts(W);
         W.n_slots = La.n;
         W.bl_rays = b->bl_rays;
         W.any_rays = b->any_rays;
@@ -1871,6 +1880,10 @@ int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounces, cons
             }
         }
         if (!any) break;
+    }
+    for (int l = 0; l < nl; l++) {  // each lane's pixels tone-mapped after its last step
+        hipLaunchKernelGGL(k_tonemap, dim3((L[l].n + threads - 1) / threads), dim3(threads), 0, L[l].s, L[l].W);
+        HIPCHK(c, hipGetLastError());
     }
     b->last_iters = 0;
     for (int l = 0; l < nl; l++) {

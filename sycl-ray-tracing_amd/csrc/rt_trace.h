@@ -780,28 +780,6 @@ RT_HD Col ct_brdf(const Mat& m, V3 L, V3 V, V3 N)  // :260-301
     return col(0.0f);
 }
 
-// ct_brdf(m, L, V, N) and ct_pdf(m, V, L, N) of one direction pair, as the reference
-// evaluates them back to back (render_kernel.cpp:607-608, :695-696): both take the half
-// vector normalize(V + L), dot(V, H) (= dot(H, V), products commute), dot(N, H) and the
-// GGX D of the same inputs, computed once here.
-RT_HD Col ct_brdf_pdf(const Mat& m, V3 L, V3 V, V3 N, float& pdf)
-{
-    V3 H = normalize(add(V, L));
-    float NoV = rt_max(0.0f, dot(N, V));
-    float NoL = rt_max(0.0f, dot(N, L));
-    float NoH = rt_max(0.0f, dot(N, H));
-    float VoH = rt_max(0.0f, dot(H, V));
-    const float alpha = m.roughness * m.roughness;
-    float D;
-    Col brdf = col(0.0f);
-    if (NoV > 0.0f && NoL > 0.0f && NoH > 0.0f)
-        brdf = ct_lobe(m, NoV, NoL, NoH, VoH, alpha, &D);
-    else
-        D = ggx_d(alpha, NoH);
-    pdf = D * NoH / (4.0f * VoH);
-    return brdf;
-}
-
 // cook_torrance_brdf_importance_sample (:392-451). out_dir is left untouched
 // when the sampled microfacet normal is below the surface.
 RT_HD Col ct_sample(const Mat& m, V3 V, V3 N, V3& out_dir, float& pdf, Rng& rng)

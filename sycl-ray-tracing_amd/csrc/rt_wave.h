@@ -66,6 +66,8 @@ struct WaveView {
     RtCamera cam;
     PixSrc src;
     int W, H, spp, bounces;
+    float cam_o[3];         // xform_point(cam, 0): every camera ray's origin (set_view_consts)
+    float aspect;           // (float)W / (float)H
     int n_slots;
     int bl_rays;            // 0: no primitive has an emissive material -> BRDF->light rays can't contribute
     int any_rays;           // 1: occlusion queries may use the any-hit walk (no analytic spheres)
@@ -212,7 +214,8 @@ RT_HD V3 xform_point(const RtCamera& c, V3 p)  // mat.cpp:94-111
     return v3(xt * w, yt * w, zt * w);
 }
 
-// framebuffer update + exposure / gamma tone-map (:167-180), in place.
+// framebuffer update + exposure / gamma tone-map (:167-180), in place (the one-step
+// form of finish_pixel + tonemap_pixel; test builds).
 RT_HD void tonemap_into(float* px, Col fin)
 {
     px[0] += fin.r;
@@ -274,9 +277,9 @@ RT_HD bool start_sample(const WaveView& W, int p, PathReg& P, Emit& e)
         float xj = ((float)x + 0.5f) + P.rng.next() - 1.0f;
         float yj = ((float)y + 0.5f) + P.rng.next() - 1.0f;
         float xn = xj / (float)W.W * 2.0f - 1.0f;
-        xn *= (float)W.W / (float)W.H;
+        xn *= W.aspect;
         float yn = yj / (float)W.H * 2.0f - 1.0f;
-        const V3 o = xform_point(W.cam, v3(0.0f, 0.0f, 0.0f));
+        const V3 o = v3(W.cam_o[0], W.cam_o[1], W.cam_o[2]);
         const V3 pd = xform_point(W.cam, v3(xn, yn, W.cam.fov_dist));
         P.ro = o;
         P.rd = normalize(sub(pd, o));
@@ -294,6 +297,17 @@ RT_HD bool start_sample(const WaveView& W, int p, PathReg& P, Emit& e)
     }
 }
 
+// The per-render constants of start_sample, evaluated once (same operations, so the
+// same values): the camera origin xform_point(cam, 0) and the aspect ratio.
+RT_HD void set_view_consts(WaveView& W)
+{
+    const V3 o = xform_point(W.cam, v3(0.0f, 0.0f, 0.0f));
+    W.cam_o[0] = o.x;
+    W.cam_o[1] = o.y;
+    W.cam_o[2] = o.z;
+    W.aspect = (float)W.W / (float)W.H;
+}
+
 // Framebuffer entry of slot p: slot rows map to every fb_rs-th framebuffer row.
 RT_HD size_t fb_at(const WaveView& W, int p)
 {
@@ -302,6 +316,12 @@ RT_HD size_t fb_at(const WaveView& W, int p)
     return (size_t)j * W.fb_rs * W.src.W + (p - j * W.src.W);
 }
 
+// The pixel's end (render_kernel.cpp:167-180) in two parts: finish_pixel adds the
+// sample average to the framebuffer when the pixel's last sample ends, and
+// tonemap_pixel (the alpha update and the exposure / gamma expf / powf of tonemap_into,
+// on the same values in the same order) runs once per pixel after the render's last
+// step, in its own converged pass (rt_render.hip k_tonemap, rt_hostsim.cpp), instead
+// of inside the divergent step code.
 RT_HD void finish_pixel(const WaveView& W, int p, PathReg& P)
 {
     const float k = (float)W.spp;
@@ -311,7 +331,25 @@ RT_HD void finish_pixel(const WaveView& W, int p, PathReg& P)
     fin.b /= k;
     float4_& dst = W.fb[fb_at(W, p)];
     float4_ px = dst;
-    tonemap_into(&px.x, fin);
+    px.x += fin.r;
+    px.y += fin.g;
+    px.z += fin.b;
+    dst = px;
+}
+
+RT_HD void tonemap_pixel(const WaveView& W, int p)
+{
+    float4_& dst = W.fb[fb_at(W, p)];
+    float4_ px = dst;
+    float* v = &px.x;
+    const float a = v[3] + 0.0f;
+    v[3] = 1.0f + (-((-a) * 1.5f));
+#pragma unroll
+    for (int c = 0; c < 3; c++) {
+        float e = rt_expf((-v[c]) * 1.5f);
+        float tm = 1.0f + (-e);
+        v[c] = rt_powf(tm, 1.0f / 2.2f);
+    }
     dst = px;
 }
 
