@@ -91,6 +91,25 @@ def _step_bytes(g) -> float:
     return BYTES["mat"] * g("mat") + BYTES["env"] * g("env") + BYTES["cdf"] * g("cdf")
 
 
+# Wavefront step model: what a path step must read besides the scene
+# records above. Per step (one continuation result consumed): the slot's 4 state
+# records (64 B), its result (8 B), live-list entry and wait count (8 B); per shaded
+# bounce: the hit triangle (48 B) and the pending throughput (16 B); per occlusion
+# query: its candidate (16 B) and answer (1 B); per sample: the fin record (16 B).
+# Exact for scenes without emissive triangles (cfg2-cfg5: every closest query is a
+# continuation and every material load a shade).
+SLOT_BYTES = {"step": 80, "shade": 64, "occ": 17, "sample": 16}
+
+
+def step_model_bytes(st: dict, samples: float) -> dict:
+    rest = lambda k: st[k] - st.get("tail_" + k, 0)  # noqa: E731
+    scene = _step_bytes(rest)
+    tail_frac = 1.0 - rest("rays") / max(st["rays"], 1)
+    slot = (SLOT_BYTES["step"] * rest("rays") + SLOT_BYTES["shade"] * rest("mat") +
+            SLOT_BYTES["occ"] * rest("any_rays") + SLOT_BYTES["sample"] * samples * (1.0 - tail_frac))
+    return {"scene": scene, "slot": slot}
+
+
 def algo_bytes(st: dict, kernel: str) -> float:
     """Algorithmic bytes of one kernel class over the counted render. The
     counters are totals over every kernel, plus the tail kernel's share
@@ -177,6 +196,15 @@ def load_traffic(key):
         return None
     e = json.load(open(p)).get(key)
     return None if e is None else e.get("bytes_per_launch")
+
+
+def load_traffic_class(key, cls):
+    """PMC FETCH_SIZE bytes per launch of one kernel class from profiles/traffic.json."""
+    p = os.path.join(REPO, "profiles", "traffic.json")
+    if not os.path.exists(p):
+        return None
+    e = json.load(open(p)).get(key)
+    return None if e is None else e.get("per_class_bytes_per_launch", {}).get(cls)
 
 
 def fail(msg: str, code: int = 2):
@@ -328,6 +356,18 @@ def main():
                     "bytes_per_sample_all_kernels": round(sum(algo_bytes(stats, k) for k in ktime) / samples_rank, 1),
                     "closest_rays_per_sample": round(stats["rays"] / samples_rank, 3),
                     "any_rays_per_sample": round(stats["any_rays"] / samples_rank, 3)}
+        # k_step against its byte models: the scene records alone (material, env texel, CDF
+        # fences) and with the wavefront's slot records; traffic = committed FETCH_SIZE pass
+        sm = step_model_bytes(stats, samples_rank)
+        s_launches = ktime["step"][1]
+        tr = load_traffic_class(f"{args.config}_1lane", "k_step") if (n_gpus == 1 and not args.sim_world) else None
+        roofline["k_step"] = {
+            "model_scene_bytes_per_launch": round(sm["scene"] / max(s_launches, 1)),
+            "model_with_slots_bytes_per_launch": round((sm["scene"] + sm["slot"]) / max(s_launches, 1)),
+            "avg_launch_ms": round(ktime["step"][0] / max(s_launches, 1), 4),
+            "traffic": tr,
+            "traffic_over_model_with_slots": round(tr / ((sm["scene"] + sm["slot"]) / max(s_launches, 1)), 3) if tr else None,
+        }
         if kernel_ms:
             # all kernels' algorithmic bytes over the timed (3-lane, overlapped) render
             roofline["render_ms"] = round(kernel_ms, 3)

@@ -1145,50 +1145,55 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TAIL_OCC
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the lists are read by other lanes
         __builtin_amdgcn_wave_barrier();
 #if RT_TAIL_MIXED
-        // trace: both lists in one index space, 16 queries (quads) per pass, each quad
-        // walking its own kind a few trips per call (rt_quad.h quad_visit): a step waits
-        // for its slowest query, not for the closest walk plus the occlusion walks after it
+        // trace: both lists in one index space, streamed over the wave's 16 quads (an idle
+        // quad takes the next query at once), each quad walking its own kind a few trips
+        // per call (rt_quad.h quad_visit): a step waits for its slowest query, not for
+        // the slowest of every 16-query pass
         const int nq = nl[0] + nl[1];
-        for (int base = 0; base < nq; base += 16) {
-            const int qi = base + (lane >> 2);
-            bool act = false, exact = false;
-            int l = 0;
-            uint32_t target = 0;
-            rtk::QState q;
-            if (qi < nq) {
-                l = qi < nl[0] ? 0 : 1;
-                const rtk::RayRec r = s_q[wv][l][l ? qi - nl[0] : qi];
-                target = rt_asuint(r.d.w);
-                q.o = rtk::v3of(r.o);
-                q.d = rtk::v3of(r.d);
-                if (forced_fallback(W, r.o, r.d)) {
-                    exact = true;
-                } else {
-                    act = l ? rtk::qstate_begin<true>(q, q.o, q.d, sub, ps) : rtk::qstate_begin<false>(q, q.o, q.d, sub, ps);
-                    if (!act && sub == 0) {  // (a NaN ray: no hit)
-                        if (l == 0)
-                            rtk::finish_closest(W, target, q.o, q.d, -1.0f, -1);
-                        else
-                            rtk::finish_any(W, target, false);
+        int next = 0;  // the next query of the lists (uniform)
+        bool act = false;
+        int l = 0;
+        uint32_t target = 0;
+        rtk::QState q;
+        for (;;) {
+            bool exact = false;
+            const unsigned long long bidle = __ballot(!act && sub == 0);
+            if (next < nq) {
+                const int qi = next + __popcll(bidle & ((1ull << (lane & ~3)) - 1ull));  // this quad's query
+                if (!act && qi < nq) {
+                    l = qi < nl[0] ? 0 : 1;
+                    const rtk::RayRec r = s_q[wv][l][l ? qi - nl[0] : qi];
+                    target = rt_asuint(r.d.w);
+                    q.o = rtk::v3of(r.o);
+                    q.d = rtk::v3of(r.d);
+                    if (forced_fallback(W, r.o, r.d)) {
+                        exact = true;
+                    } else {
+                        act = l ? rtk::qstate_begin<true>(q, q.o, q.d, sub, ps) : rtk::qstate_begin<false>(q, q.o, q.d, sub, ps);
+                        if (!act && sub == 0) {  // (a NaN ray: no hit)
+                            if (l == 0)
+                                rtk::finish_closest(W, target, q.o, q.d, -1.0f, -1);
+                            else
+                                rtk::finish_any(W, target, false);
+                        }
                     }
                 }
+                next = min(nq, next + __popcll(bidle));
             }
-            while (__any(act)) {
-                if (act) {
-                    const int res = l ? rtk::quad_visit<true>(S, q, stk, sub, ps) : rtk::quad_visit<false>(S, q, stk, sub, ps);
-                    if (res != 0) {
-                        act = false;
-                        float t = 0.0f;
-                        int k = 0;
-                        const bool ok = res > 0 && (l == 1 || rtk::quad_closest_answer(S, q, sub, t, k, ps));
-                        if (ok && sub == 0) {
-                            if (l == 0)
-                                rtk::finish_closest(W, target, q.o, q.d, t, k);
-                            else
-                                rtk::finish_any(W, target, q.h.k == 1);
-                        }
-                        exact = !ok;
+            if (act) {
+                const int res = l ? rtk::quad_visit<true>(S, q, stk, sub, ps) : rtk::quad_visit<false>(S, q, stk, sub, ps);
+                if (res != 0) {
+                    act = false;
+                    float t = 0.0f;
+                    int k = 0;
+                    const bool ok = res > 0 && (l == 1 || rtk::quad_closest_answer(S, q, sub, t, k, ps));
+                    if (ok && sub == 0) {
+                        if (l == 0)
+                            rtk::finish_closest(W, target, q.o, q.d, t, k);
+                        else
+                            rtk::finish_any(W, target, q.h.k == 1);
                     }
+                    exact = !ok;
                 }
             }
             if (exact && sub == 0) {  // the exact octree walk, to completion
@@ -1208,6 +1213,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TAIL_OCC
                     rtk::finish_any(W, target, T.hit);
                 }
             }
+            if (next >= nq && !__any(act)) break;
         }
         if (probe) {
             const long long t2 = wall_clock64();
