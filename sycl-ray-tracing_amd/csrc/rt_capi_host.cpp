@@ -35,6 +35,7 @@ RtSceneView rt_host_view(const rt_context* c)
     v.prim2k = c->flat.prim2k.data();
     v.mat_idx = c->mat_idx.data();
     v.mats = c->mats.data();
+    v.n_mats = (int)c->mats.size();
     v.emissive = c->emissive.data();
     v.spheres = c->spheres.data();
     v.env = c->env.data();

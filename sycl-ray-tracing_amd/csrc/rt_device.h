@@ -92,6 +92,7 @@ struct RtSceneView {
     int32_t n_emissive, n_spheres, ew, eh;
     int32_t n_tris, chain_monotone, cdf_cw;  // chain_monotone: see rt_fast.h chain_ok
     float cdf_total;  // cdf[ew * eh - 1] (render_kernel.cpp:572, :619), a parameter instead of a load
+    int32_t n_mats;   // entries of mats
     int32_t brute;  // 1: INTERSECT_SCENE is the brute-force loop (USE_BVH 0, render_kernel.cpp:453-483)
     // search BVH + octree back-links for the verification walk
     const Bvh4Node* bvh4;      // [0] = root

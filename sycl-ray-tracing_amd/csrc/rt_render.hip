@@ -611,6 +611,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_STEP_OCC
     __shared__ uint32_t s_lds[RT_LDS_WORDS * 256];
     __shared__ int s_pre[RT_QSHARDS + 1];
     rtlibm::lds_tables_init();
+    rtk::lds_shade_init(W.S);  // (the env-map row search and a small material table from LDS)
     int32_t* cnt = W.counters;
     if (blockIdx.x == 0 && threadIdx.x == 0) {  // for k_trace(i + 1); DONE[par ^ 1] was released by k_trace(i)
         cnt[C_FBC0 + (par ^ 1)] = cnt[C_FBA0 + (par ^ 1)] = 0;
@@ -1074,6 +1075,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TAIL_OCC
     __shared__ uint32_t s_stk[2 * RT_QSTACK * 64];
     __shared__ int s_pre[RT_QSHARDS + 1];
     rtlibm::lds_tables_init();
+    rtk::lds_shade_init(W.S);  // (the env-map row search and a small material table from LDS)
     int32_t* cnt = W.counters;
     shard_prefix(cnt, RT_QSHARDS, [&](int j) { return ac_at(par, j); }, s_pre);
     const int n = s_pre[RT_QSHARDS];
@@ -1513,6 +1515,7 @@ int upload_one(rt_context* c, Backend* b, const std::vector<int32_t>& matk, bool
     if (mats_only) {  // rt_set_materials: the material table (and what depends on it) alone
         if ((r = upload(c, b->mats, c->mats))) return r;
         b->view.mats = (const RtMat*)b->mats.p;
+        b->view.n_mats = (int)c->mats.size();
         b->bl_rays = rt_scene_has_emissive_prim(c) ? 1 : 0;
         return RT_OK;
     }
@@ -1539,6 +1542,7 @@ int upload_one(rt_context* c, Backend* b, const std::vector<int32_t>& matk, bool
     v.mat_idx = (const int32_t*)b->mat_idx.p;
     v.matk = (const int32_t*)b->matk.p;
     v.mats = (const RtMat*)b->mats.p;
+    v.n_mats = (int)c->mats.size();
     v.emissive = (const int32_t*)b->emissive.p;
     v.spheres = (const float4_*)b->spheres.p;
     v.env = (const float4_*)b->env.p;

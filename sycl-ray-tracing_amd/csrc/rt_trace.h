@@ -694,16 +694,29 @@ struct Mat {
     Col emission, diffuse;
     float metalness, roughness;
 };
+// A material record: from the LDS copy when the shading kernel staged the table
+// (lds_shade_init, n_mats <= RT_MAT_LDS), else from memory.
+#define RT_MAT_LDS 64
+#if defined(__HIPCC__)
+__shared__ RtMat rt_mat_lds[RT_MAT_LDS];
+#endif
+RT_HD RtMat mat_rec(const RtSceneView& S, int i)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    if (S.n_mats <= RT_MAT_LDS) return rt_mat_lds[i];
+#endif
+    return S.mats[i];
+}
 RT_HD Mat load_mat(const RtSceneView& S, int prim)
 {
-    const RtMat m = S.mats[S.mat_idx[prim]];
+    const RtMat m = mat_rec(S, S.mat_idx[prim]);
     return Mat{Col{m.er, m.eg, m.eb}, Col{m.dr, m.dg, m.db}, m.metalness, m.roughness};
 }
 // The material of a hit: for a triangle (leaf-order k >= 0) through matk[k],
 // the same entry as mat_idx[prim] (built at upload), without the dependent load.
 RT_HD Mat load_mat_hit(const RtSceneView& S, int k, int prim)
 {
-    const RtMat m = S.mats[(k >= 0 && S.matk) ? S.matk[k] : S.mat_idx[prim]];
+    const RtMat m = mat_rec(S, (k >= 0 && S.matk) ? S.matk[k] : S.mat_idx[prim]);
     return Mat{Col{m.er, m.eg, m.eb}, Col{m.dr, m.dg, m.db}, m.metalness, m.roughness};
 }
 // The material of a hit record (its material index already read with the triangle when
@@ -711,7 +724,7 @@ RT_HD Mat load_mat_hit(const RtSceneView& S, int k, int prim)
 RT_HD Mat load_mat_of(const RtSceneView& S, const Hit& h)
 {
     if (h.mi < 0) return load_mat_hit(S, h.k, h.prim);
-    const RtMat m = S.mats[h.mi];
+    const RtMat m = mat_rec(S, h.mi);
     return Mat{Col{m.er, m.eg, m.eb}, Col{m.dr, m.dg, m.db}, m.metalness, m.roughness};
 }
 
@@ -862,9 +875,42 @@ RT_HD int fence_count(const float* a, const float* t, int m, float value)
     return fence_level(a, c, 1, m, value);
 }
 
+// The row search's fence table and row ends staged in LDS by the shading kernels
+// (lds_cdf_init: k_step, k_tail), so three of the search's six dependent loads are LDS
+// reads. RT_CDF_LDS 0: every level from global memory.
+#ifndef RT_CDF_LDS
+#define RT_CDF_LDS 1
+#endif
+#define RT_CDF_LDS_ROWS 1024
+#if defined(__HIPCC__) && RT_CDF_LDS
+__shared__ float4_ rt_cdf_lds[(272 + RT_CDF_LDS_ROWS) / 4];  // fence table 0 (272), then cdf_row
+#endif
+#if defined(__HIPCC__)
+// The shading kernels' LDS copies (k_step, k_tail; whole block, ends with a barrier).
+__device__ __forceinline__ void lds_shade_init(const RtSceneView& S)
+{
+#if RT_CDF_LDS
+    if (S.cdf_fence && S.eh <= RT_CDF_LDS_ROWS) {
+        float* t = (float*)rt_cdf_lds;
+        for (int i = (int)threadIdx.x; i < 272 + S.eh; i += (int)blockDim.x)
+            t[i] = i < 272 ? S.cdf_fence[i] : S.cdf_row[i - 272];
+    }
+#endif
+    if (S.n_mats <= RT_MAT_LDS)
+        for (int i = (int)threadIdx.x; i < S.n_mats; i += (int)blockDim.x) rt_mat_lds[i] = S.mats[i];
+    __syncthreads();
+}
+#endif
+
 RT_HD void cdf_search(const RtSceneView& S, float value, int& x, int& y, Stats* st)  // :532-567
 {
     if (S.cdf_fence) {
+#if defined(__HIP_DEVICE_COMPILE__) && RT_CDF_LDS
+        if (S.eh <= RT_CDF_LDS_ROWS) {
+            const float* t = (const float*)rt_cdf_lds;
+            y = fence_count(t + 272, t, S.eh - 1, value);
+        } else
+#endif
         y = fence_count(S.cdf_row, S.cdf_fence, S.eh - 1, value);
         x = fence_count(S.cdf + (size_t)y * S.ew, S.cdf_fence + (size_t)(1 + y) * 272, S.ew - 1, value);
         if (st) st->c[RT_STAT_CDF] += 6;  // six 64-B fence loads
