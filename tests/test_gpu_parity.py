@@ -147,6 +147,32 @@ def test_gpu_random_configs_match_oracle(cameras):
             assert_parity(fb.pixels, want, min_bitwise=1.0)
 
 
+@pytest.mark.gpu
+def test_gpu_many_materials_match_oracle(cameras):
+    """A material table larger than the shading kernels stage in LDS (> 64
+    entries: the global-memory path): the Cornell box with its 9 materials
+    repeated 9 times and triangle t using copy t % 9, against the oracle on
+    the same buffers (and so the same image as the plain box)."""
+    from oracle_bindings import OracleScene
+    P = parsed_scene("cornell")
+    k = 9
+    nm = len(P.materials)
+    mats = np.tile(P.materials, (k, 1))
+    mi = (P.material_indices + nm * (np.arange(len(P.material_indices)) % k)).astype(P.material_indices.dtype)
+    assert len(mats) > 64
+    sky = rt_cases.sky("S")
+    S = OracleScene(P.triangles, mi, mats, P.emissive_triangle_indices, env=sky)
+    W, H, spp, nb = 96, 72, 4, 5
+    want, _ = S.render(cameras["cornell"], W, H, spp, nb)
+    fb = rt_amd.Image(W, H)
+    rk = rt_amd.RenderKernel(W, H, spp, nb, fb, P.triangles, mats, P.emissive_triangle_indices, mi, None,
+                             rt_amd.BVH(P.triangles), rt_amd.Image.from_rgb(sky), None)
+    c = cameras["cornell"]
+    rk.set_camera(rt_amd.Camera(c[:16], c[16]))
+    rk.render()
+    assert_parity(fb.pixels, want, min_bitwise=1.0)
+
+
 # ------------------------------------------------------------ device libm
 _FN = {0: "expf", 2: "sinf", 3: "cosf", 4: "acosf", 5: "asinf"}
 
@@ -239,17 +265,19 @@ def test_gpu_slab_division_exact():
 
 def test_gpu_schedules_bit_identical(monkeypatch):
     """The frame does not depend on the schedule: 1-4 wavefront lanes, the
-    tail kernel on or off, and row shards split across lanes (framebuffer row
-    pitch) all give the same bits as one lane without the tail kernel."""
+    tail kernel on or off, row shards split across lanes (framebuffer row
+    pitch) and k_trace's heavy class (off, every walk heavy, the default) all
+    give the same bits as one lane without the tail kernel."""
     import scenes
     from hip_mem import DeviceBuffer
     P = rt_amd.parse_obj(scenes.scene_path("dragon_small"))
     sky = scenes.make_sky("L")
     W, H, spp, nb = 640, 480, 2, 8
 
-    def render(lanes, tail, off=0, stride=1):
+    def render(lanes, tail, off=0, stride=1, heavy=6):
         monkeypatch.setenv("RT_LANES", str(lanes))
         monkeypatch.setenv("RT_TAIL_PATHS", str(tail))
+        monkeypatch.setenv("RT_HEAVY", str(heavy))
         rk = rt_amd.RenderKernel(W, H, spp, nb, rt_amd.Image(1, 1), P.triangles, P.materials,
                                  P.emissive_triangle_indices, P.material_indices, None, rt_amd.BVH(P.triangles),
                                  rt_amd.Image.from_rgb(sky), None, device=0)
@@ -270,6 +298,9 @@ def test_gpu_schedules_bit_identical(monkeypatch):
     for off in (0, 1):
         got = render(3, 4, off, 2)
         np.testing.assert_array_equal(got.view(np.uint32), base[off::2].view(np.uint32), err_msg=f"shard {off}/2")
+    for heavy in (0, 1):  # heavy class off / every path's rays in the heavy shards
+        got = render(3, 4, heavy=heavy)
+        np.testing.assert_array_equal(got.view(np.uint32), base.view(np.uint32), err_msg=f"heavy={heavy}")
 
 
 @pytest.mark.gpu
