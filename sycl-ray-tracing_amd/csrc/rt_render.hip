@@ -1062,6 +1062,63 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_OC
 // walk, so every path is ready to step; a query the quad walk cannot answer
 // is answered here by the exact walk, inline, by lane 0 of its quad.
 #define RT_TAIL_MAXP 16  // paths per wave at most (5 rays each: 80 per list)
+// k_tail: a path's emitted rays -> the wave's LDS lists (l0: closest-hit kinds, l1: occlusion)
+__device__ __forceinline__ void tail_lists(const rtk::Emit& e, int last_kind, rtk::RayRec* l0, rtk::RayRec* l1, int* nl)
+{
+    const int lane = lane_id();
+    nl[0] = nl[1] = 0;
+#pragma unroll
+    for (int k = 0; k < rtk::RK_COUNT; k++) {
+        const bool want = (e.mask >> k) & 1u;
+        const unsigned long long b = __ballot(want);
+        const int l = k <= last_kind ? 0 : 1;
+        if (want) {
+            const int pos = nl[l] + __popcll(b & ((1ull << lane) - 1ull));
+            rtk::RayRec r = e.r[k];
+            r.d.w = rt_asfloat((rt_asuint(r.o.w) << 3) | (uint32_t)k);
+            (l ? l1 : l0)[pos] = r;
+        }
+        nl[l] += __popcll(b);
+    }
+}
+#ifndef RT_TAIL_STEP_CALL
+#define RT_TAIL_STEP_CALL 1  // k_tail's path step out of line (its registers apart from the walk loop's): cfg2 811 -> 828 Msamples/s, cfg4 8-way shard 436 -> 403 ms
+#endif
+// k_tail's path step (lanes with my >= 0) and list append, out of line: bit 0 the lane's
+// path stays in flight, bits 1-10 / 11- the closest / occlusion list lengths.
+__device__ __noinline__ int tail_step(const rtk::WaveView& W, int my, int last_kind, rtk::RayRec* l0, rtk::RayRec* l1,
+                                      rtk::Stats* ps)
+{
+    rtk::Emit e;
+    e.mask = 0;
+    e.active = false;
+    e.heavy = false;
+    if (my >= 0) rtk::path_step(W, my, e, ps);
+    int nl[2];
+    tail_lists(e, last_kind, l0, l1, nl);
+    return (e.active ? 1 : 0) | (nl[0] << 1) | (nl[1] << 11);
+}
+// k_tail's inline exact walk (a query the quad walk cannot settle: ~1e-6 of them), kept
+// out of line so that its registers do not add to the tail loop's: inlined, k_tail
+// needed 468 VGPR spill slots at its 168-VGPR budget, out of line ~190.
+template <class XS>
+__device__ __noinline__ void tail_exact(const rtk::WaveView& W, int l, uint32_t target, rtk::V3 o, rtk::V3 d, XS& xs,
+                                        rtk::Stats* ps)
+{
+    if (l == 0) {
+        rtk::TravC T;
+        if (rtk::travc_begin(W.S, T, o, d, ps))
+            while (rtk::travc_step(W.S, T, xs, ps)) {
+            }
+        rtk::finish_closest(W, target, T.o, T.d, T.best_t, T.best_k);
+    } else {
+        rtk::TravA T;
+        if (rtk::trava_begin(W.S, T, o, d, ps))
+            while (rtk::trava_step(W.S, T, xs, ps)) {
+            }
+        rtk::finish_any(W, target, T.hit);  // (begin leaves the brute-force answer in T.hit)
+    }
+}
 #ifndef RT_TAIL_MIXED
 #define RT_TAIL_MIXED 1  // closest and occlusion queries of a step in one pass (quad_query_mixed)
 #endif
@@ -1114,35 +1171,33 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TAIL_OCC
         }
         if (!__any(my >= 0)) break;
         rounds++;
-        // step
-        rtk::Emit e;
-        e.mask = 0;
-        e.active = false;
-        e.heavy = false;
+        // step; the emitted rays -> the wave's LDS lists
         const long long t0 = probe ? wall_clock64() : 0;
-        if (my >= 0) {
-            rtk::path_step(W, my, e, ps);
-            if (!e.active) my = -1;
+        int nl[2];
+#if RT_TAIL_STEP_CALL
+        {
+            const int r = tail_step(W, my, last_kind, s_q[wv][0], s_q[wv][1], ps);
+            if (!(r & 1)) my = -1;
+            nl[0] = (r >> 1) & 0x3ff;
+            nl[1] = r >> 11;
         }
+#else
+        {
+            rtk::Emit e;
+            e.mask = 0;
+            e.active = false;
+            e.heavy = false;
+            if (my >= 0) {
+                rtk::path_step(W, my, e, ps);
+                if (!e.active) my = -1;
+            }
+            tail_lists(e, last_kind, s_q[wv][0], s_q[wv][1], nl);
+        }
+#endif
         long long t1 = 0;
         if (probe) {
             t1 = wall_clock64();
             tk_step += __shfl(t1, 0) - __shfl(t0, 0);
-        }
-        // emitted rays -> the wave's LDS lists
-        int nl[2] = {0, 0};
-#pragma unroll
-        for (int k = 0; k < rtk::RK_COUNT; k++) {
-            const bool want = (e.mask >> k) & 1u;
-            const unsigned long long b = __ballot(want);
-            const int l = k <= last_kind ? 0 : 1;
-            if (want) {
-                const int pos = nl[l] + __popcll(b & ((1ull << lane) - 1ull));
-                rtk::RayRec r = e.r[k];
-                r.d.w = rt_asfloat((rt_asuint(r.o.w) << 3) | (uint32_t)k);
-                s_q[wv][l][pos] = r;
-            }
-            nl[l] += __popcll(b);
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the lists are read by other lanes
         __builtin_amdgcn_wave_barrier();
@@ -1201,19 +1256,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TAIL_OCC
             if (exact && sub == 0) {  // the exact octree walk, to completion
                 if (STATS) st.c[RT_STAT_FALLBACK]++;
                 xs.f = stk;
-                if (l == 0) {
-                    rtk::TravC T;
-                    if (rtk::travc_begin(W.S, T, q.o, q.d, ps))
-                        while (rtk::travc_step(W.S, T, xs, ps)) {
-                        }
-                    rtk::finish_closest(W, target, T.o, T.d, T.best_t, T.best_k);
-                } else {
-                    rtk::TravA T;
-                    if (rtk::trava_begin(W.S, T, q.o, q.d, ps))
-                        while (rtk::trava_step(W.S, T, xs, ps)) {
-                        }
-                    rtk::finish_any(W, target, T.hit);
-                }
+                tail_exact(W, l, target, q.o, q.d, xs, ps);
             }
             if (next >= nq && !__any(act)) break;
         }
