@@ -24,6 +24,7 @@ run() { # name, rocprof args...
 }
 run trace --kernel-trace --stats --output-format csv rocpd || exit 1
 run pmc_fetch --pmc FETCH_SIZE || exit 1
+run pmc_write --pmc WRITE_SIZE || exit 1
 # occupancy / issue / wait counters of the same command (one pass each)
 if [ -n "$PMC_DETAIL" ]; then
   run pmc_a --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU || exit 1

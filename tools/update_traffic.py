@@ -1,0 +1,53 @@
+"""Writes profiles/traffic.json's `<config>_1lane` entry from a tools/profile_roofline.sh
+run: FETCH_SIZE / WRITE_SIZE of the non-stats (<false>) dispatches, which are the two
+1-lane renders of `bench.py --roofline-only`, per dispatch. FETCH KB x 1024 x 2 (the
+gfx950 FETCH_SIZE correction of /opt/skills/guides/MI355X_MICROARCH.md), WRITE KB x 1024.
+
+  python tools/update_traffic.py ROOF_DIR [--config cfg2] [--build COMMIT]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def per_launch(path, counter, scale):
+    d = json.load(open(path))
+    out = {}
+    for k in ("k_trace", "k_step", "k_tail"):
+        r = d.get(f"{k}<false>")
+        if r and r.get("dispatches"):
+            out[k] = int(round(r[counter] * 1024 * scale / r["dispatches"]))
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("roof_dir")
+    ap.add_argument("--config", default="cfg2")
+    ap.add_argument("--build", default="")
+    args = ap.parse_args()
+    fetch = per_launch(os.path.join(args.roof_dir, "pmc_fetch.json"), "FETCH_SIZE", 2)
+    write = per_launch(os.path.join(args.roof_dir, "pmc_write.json"), "WRITE_SIZE", 1)
+    p = os.path.join(REPO, "profiles", "traffic.json")
+    t = json.load(open(p)) if os.path.exists(p) else {}
+    rel = os.path.relpath(args.roof_dir, REPO)
+    t[f"{args.config}_1lane"] = {
+        "bytes_per_launch": fetch["k_trace"],
+        "per_class_bytes_per_launch": fetch,
+        "per_class_write_bytes_per_launch": write,
+        "source": f"{rel}/pmc_fetch.json (FETCH_SIZE) and pmc_write.json (WRITE_SIZE): rocprofv3 --pmc over "
+                  f"`bench.py --roofline-only --no-cpu-baseline --config {args.config}` (tools/profile_roofline.sh; "
+                  "the <false> dispatches are the two 1-lane renders); FETCH KB x1024 x2 (gfx950 correction, "
+                  "MI355X_MICROARCH.md), WRITE KB x1024, / dispatches" + (f"; build of commit {args.build}" if args.build else ""),
+        "round": 2,
+    }
+    json.dump(t, open(p, "w"), indent=1)
+    print(json.dumps(t[f"{args.config}_1lane"]))
+
+
+if __name__ == "__main__":
+    main()
