@@ -437,12 +437,12 @@ __device__ __forceinline__ bool qstate_begin(QState& q, V3 o, V3 d, int sub, Sta
 #define RT_VISIT_DESCEND 2  // inner-node trips a quad_visit call may take in a row before returning
                             // (cfg2, refill 8: 1 / 2 / 4 -> 680 / 725 / 706 Msamples/s)
 #endif
-template <bool ANY, class QSTK>
+template <bool ANY, int DESC = RT_VISIT_DESCEND, class QSTK>
 __device__ __forceinline__ int quad_visit(const RtSceneView& S, QState& q, QSTK& stk, int sub, Stats* st)
 {
     FastHit& h = q.h;
 #pragma unroll 1
-    for (int dd = 0; dd < RT_VISIT_DESCEND && q.cur >= 0; dd++) {
+    for (int dd = 0; dd < DESC && q.cur >= 0; dd++) {
         if (st && sub == 0) st->c[ANY ? RT_STAT_ANY_VOL : RT_STAT_VOL] += 4;
         const float tmax = ANY ? __builtin_inff() : h.t + h.t * RT_T2_WINDOW;
         const QChild c = quad_child(S, q.cur, sub, q.rb, tmax);
@@ -477,7 +477,7 @@ __device__ __forceinline__ int quad_visit(const RtSceneView& S, QState& q, QSTK&
         q.cur = 0x7ffffffe;
         break;
     }
-    if (q.cur >= 0 && q.cur != 0x7ffffffe) return 0;  // (descended RT_VISIT_DESCEND times; still inner)
+    if (q.cur >= 0 && q.cur != 0x7ffffffe) return 0;  // (descended DESC times; still inner)
     if (q.cur < 0) {
         if (st && sub == 0) st->c[ANY ? RT_STAT_ANY_TRI : RT_STAT_TRI] += ((~q.cur) & 3) + 1;
         int k, leaf, prim;

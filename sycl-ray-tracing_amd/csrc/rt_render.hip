@@ -1122,6 +1122,9 @@ __device__ __noinline__ void tail_exact(const rtk::WaveView& W, int l, uint32_t 
 #ifndef RT_TAIL_MIXED
 #define RT_TAIL_MIXED 1  // closest and occlusion queries of a step in one pass (quad_query_mixed)
 #endif
+#ifndef RT_TAIL_DESCEND
+#define RT_TAIL_DESCEND RT_VISIT_DESCEND  // inner-node trips per quad_visit call in k_tail
+#endif
 #ifndef RT_TAIL_OCC
 #define RT_TAIL_OCC 3    // k_tail waves per SIMD (2: no spills but half the paths per launch; 3 measured faster)
 #endif
@@ -1238,7 +1241,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TAIL_OCC
                 next = min(nq, next + __popcll(bidle));
             }
             if (act) {
-                const int res = l ? rtk::quad_visit<true>(S, q, stk, sub, ps) : rtk::quad_visit<false>(S, q, stk, sub, ps);
+                const int res = l ? rtk::quad_visit<true, RT_TAIL_DESCEND>(S, q, stk, sub, ps)
+                                  : rtk::quad_visit<false, RT_TAIL_DESCEND>(S, q, stk, sub, ps);
                 if (res != 0) {
                     act = false;
                     float t = 0.0f;
