@@ -452,7 +452,7 @@ __device__ __forceinline__ int quad_visit(const RtSceneView& S, QState& q, QSTK&
             const int pre = (s_lower(sub, 1) ? o1 : 0) + (s_lower(sub, 2) ? o2 : 0) + (s_lower(sub, 3) ? o3 : 0);
             const int nv = okb + o1 + o2 + o3;
             if (q.sp + nv - 1 > QSTK::CAP) return -1;
-            if (c.ok && pre > 0) stk.set(q.sp + pre - 1, (uint32_t)c.item, 0.0f);
+            if (c.ok && pre > 0) stk.set_rec(q.sp + pre - 1, (uint32_t)c.item);  // (an occlusion walk never reads keys)
             if (nv > 0) {
                 q.sp += nv - 1;
                 q.cur = qor(c.ok && pre == 0 ? c.item : 0);
