@@ -418,8 +418,9 @@ __global__ __launch_bounds__(256) void k_tonemap(rtk::WaveView W)
 #define RT_LDS_CAP_ANY 16
 #define RT_REFILL 16
 #define RT_QSTACK 32            // quad walks (rt_quad.h): stack entries per quad (item + key, 64 quads per block)
-#ifndef RT_TRACE_STEAL
-#define RT_TRACE_STEAL 0        // occlusion walks shared by idle quads once a wave's stream has run out
+#ifndef RT_COOP_LIVE
+#define RT_COOP_LIVE -1         // occlusion walks shared by idle quads once a wave's stream has run out, in the
+                                // k_trace launches of at most this many live paths (-1: never)
 #endif
 #ifndef RT_TRACE_REFILL
 #define RT_TRACE_REFILL 4       // k_trace: idle quads of a wave that trigger a refill from its query stream (0: static
@@ -743,7 +744,7 @@ __device__ __forceinline__ void trace_stream(const rtk::WaveView& W, const RtSce
     }
 }
 
-// k_trace's occlusion role with cooperative drains (RT_TRACE_STEAL): as trace_stream<true>,
+// k_trace's occlusion role with cooperative drains (k_trace<., true>): as trace_stream<true>,
 // and once the wave's stream has run out an idle quad takes the OLDEST stack entry of a
 // walk that still has two or more and walks that subtree for it (the occlusion answer
 // does not depend on the visit order): an occluder found by either ends both; the walk
@@ -886,14 +887,13 @@ __device__ __forceinline__ void trace_stream_any_coop(const rtk::WaveView& W, co
     }
 }
 
-template <bool STATS>
+// COOP: the occlusion role with cooperative drains (trace_stream_any_coop); the host picks
+// it for the launches of few queries, where the drain is most of the launch (RT_COOP_LIVE)
+template <bool STATS, bool COOP>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_OCC, 8))) void k_trace(rtk::WaveView W, int par, unsigned long long* stats)
 {
     __shared__ uint32_t s_lds[RT_LDS_WORDS * 256];
     __shared__ int s_pre[RT_NSEG + 1];
-#if RT_TRACE_STEAL
-    __shared__ int s_coop[9 * 64];
-#endif
     int32_t* cnt = W.counters;
     if (blockIdx.x == 0) {  // filled by k_step(i) next
         for (int j = threadIdx.x; j < (rtk::RK_COUNT + 1) * RT_QSHARDS; j += blockDim.x)
@@ -946,14 +946,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_OC
     // RT_TRACE_REFILL quads are idle they all take the next queries, so a long walk holds
     // up its own quad, not the wave's next 15 queries. Same trips and answers as the
     // whole-walk functions.
-    if (closest)
+    if (closest) {
         trace_stream<false, STATS>(W, S, stk, s_pre, c0, total, wg, wn, fbn, fbl, ps);
-    else
-#if RT_TRACE_STEAL
+    } else if (COOP) {
+        __shared__ int s_coop[9 * 64];
         trace_stream_any_coop<STATS>(W, S, stk, s_pre, a0, total, wg, wn, fbn, fbl, s_coop, ps);
-#else
+    } else {
         trace_stream<true, STATS>(W, S, stk, s_pre, a0, total, wg, wn, fbn, fbl, ps);
-#endif
+    }
 #else
     const int sub = (int)(threadIdx.x & 3);
     for (int base = wg * 16; base < total; base += wn * 16) {
@@ -1742,6 +1742,8 @@ int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounces, cons
     if (const char* e = getenv("RT_FORCE_FALLBACK")) force_fb = std::max(0, atoi(e));
     int heavy_calls = RT_HEAVY_CALLS;
     if (const char* e = getenv("RT_HEAVY")) heavy_calls = std::max(0, atoi(e));
+    long coop_live = RT_COOP_LIVE;  // k_trace launches of at most this many live paths use the cooperative drain
+    if (const char* e = getenv("RT_COOP_LIVE")) coop_live = atol(e);
     int tail_p = 5;  // (5 paths: 15 queries, one pass of the wave's 16 quads; sweep 2-6 within 1 %)
     if (const char* e = getenv("RT_TAIL_PATHS")) tail_p = std::min(RT_TAIL_MAXP, std::max(0, atoi(e)));
     const int tail_blocks = dev_cus * RT_TAIL_OCC;  // one grid-fill of k_tail
@@ -1845,10 +1847,15 @@ int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounces, cons
             for (int k = 0; k < 3; k++)
                 if (!La.tev[k][La.it]) HIPCHK(c, hipEventCreate(&La.tev[k][La.it]));
         if (T) HIPCHK(c, hipEventRecord(La.tev[0][La.it], La.s));
-        if (S)
-            hipLaunchKernelGGL(k_trace<true>, dim3(trace_blocks_of(La)), dim3(threads), 0, La.s, W, par, stats);
+        const bool coop = La.live <= coop_live;
+        if (S && coop)
+            hipLaunchKernelGGL((k_trace<true, true>), dim3(trace_blocks_of(La)), dim3(threads), 0, La.s, W, par, stats);
+        else if (S)
+            hipLaunchKernelGGL((k_trace<true, false>), dim3(trace_blocks_of(La)), dim3(threads), 0, La.s, W, par, stats);
+        else if (coop)
+            hipLaunchKernelGGL((k_trace<false, true>), dim3(trace_blocks_of(La)), dim3(threads), 0, La.s, W, par, stats);
         else
-            hipLaunchKernelGGL(k_trace<false>, dim3(trace_blocks_of(La)), dim3(threads), 0, La.s, W, par, stats);
+            hipLaunchKernelGGL((k_trace<false, false>), dim3(trace_blocks_of(La)), dim3(threads), 0, La.s, W, par, stats);
         if (T) HIPCHK(c, hipEventRecord(La.tev[1][La.it], La.s));
         HIPCHK(c, hipGetLastError());
         return RT_OK;

@@ -18,9 +18,11 @@ def per_launch(path, counter, scale):
     d = json.load(open(path))
     out = {}
     for k in ("k_trace", "k_step", "k_tail"):
-        r = d.get(f"{k}<false>")
-        if r and r.get("dispatches"):
-            out[k] = int(round(r[counter] * 1024 * scale / r["dispatches"]))
+        # every non-stats instantiation (<false> or <false, ...>)
+        rs = [r for name, r in d.items() if name == f"{k}<false>" or name.startswith(f"{k}<false,")]
+        n = sum(r.get("dispatches", 0) for r in rs)
+        if n:
+            out[k] = int(round(sum(r[counter] for r in rs) * 1024 * scale / n))
     return out
 
 
