@@ -147,7 +147,7 @@ RT_HD void sort4(float* k, int* v)
 
 // Relative width of the window past t* in which other hits are collected.
 #ifndef RT_T2_WINDOW
-#define RT_T2_WINDOW 1.0e-3f
+#define RT_T2_WINDOW 1.0e-5f  // (cfg2 r02: 1e-3 / 1e-4 / 1e-5 -> closest box tests 3.571 / 3.544 / 3.540 G, fallbacks 375 each; 828-832 / 833 / 833-836 Msamples/s)
 #endif
 
 // Search-BVH walk: 1 = one item (node or leaf) per trip (fast_closest_u /
