@@ -1,7 +1,7 @@
 #!/bin/bash
 # The roofline command under rocprofv3 (GPU box): `bench.py --roofline-only` renders
 # the frame once with the stats kernels (counter pass), then twice with ONE lane
-# (warm + timed), so the k_trace<false> dispatches in these profiles are exactly
+# (warm + timed), so the k_trace<false, false> dispatches in these profiles are exactly
 # the 1-lane launches whose mean duration bench.py's roofline line reports.
 # Usage: tools/profile_roofline.sh OUTDIR [bench args...]
 set -o pipefail
