@@ -437,12 +437,71 @@ __device__ __forceinline__ bool qstate_begin(QState& q, V3 o, V3 d, int sub, Sta
 #define RT_VISIT_DESCEND 2  // inner-node trips a quad_visit call may take in a row before returning
                             // (cfg2, refill 8: 1 / 2 / 4 -> 680 / 725 / 706 Msamples/s)
 #endif
+#ifndef RT_ANY_PAIR
+#define RT_ANY_PAIR 1  // occlusion walks: an inner trip also takes the stack top's node (8 boxes per round trip;
+                       // cfg2 850-858 vs 834-835 Msamples/s, quad visits -6 %, cfg4 8-way shard 411 -> 402 ms)
+#endif
+// Lane sub's children of two inner nodes (a, and b when pair), both records loaded
+// before either is tested: one memory round trip. Occlusion walks (no window).
+__device__ __forceinline__ void quad_child2(const RtSceneView& S, int a, int b, bool pair, int sub, const RayB& rb,
+                                            QChild& ca, QChild& cb)
+{
+    float4_ a0, a1, b0 = float4_{0.0f, 0.0f, 0.0f, 0.0f}, b1 = b0;
+    child_record(S, a, sub, a0, a1);
+    if (pair) child_record(S, b, sub, b0, b1);
+    rt_pin(a0);
+    rt_pin(a1);
+    rt_pin(b0);
+    rt_pin(b1);
+    {
+        const int ref = (int)rt_asuint(a1.z), cnt = (int)rt_asuint(a1.w);
+        const float mn[3] = {a0.x, a0.y, a0.z}, mx[3] = {a0.w, a1.x, a1.y};
+        ca.ok = cnt >= 0 && box_hit(mn, mx, rb, __builtin_inff(), ca.tn);
+        ca.item = cnt > 0 ? leaf_item(ref, cnt) : ref;
+    }
+    {
+        const int ref = (int)rt_asuint(b1.z), cnt = (int)rt_asuint(b1.w);
+        const float mn[3] = {b0.x, b0.y, b0.z}, mx[3] = {b0.w, b1.x, b1.y};
+        cb.ok = pair && cnt >= 0 && box_hit(mn, mx, rb, __builtin_inff(), cb.tn);
+        cb.item = cnt > 0 ? leaf_item(ref, cnt) : ref;
+    }
+}
+
 template <bool ANY, int DESC = RT_VISIT_DESCEND, class QSTK>
 __device__ __forceinline__ int quad_visit(const RtSceneView& S, QState& q, QSTK& stk, int sub, Stats* st)
 {
     FastHit& h = q.h;
 #pragma unroll 1
     for (int dd = 0; dd < DESC && q.cur >= 0; dd++) {
+        if (ANY && RT_ANY_PAIR) {
+            // the stack top, when it is an inner node, is walked in the same trip (the
+            // occlusion answer does not depend on the visit order)
+            int b = -1;
+            if (q.sp > q.bot) b = (int)stk.rec(q.sp - 1);
+            const bool pair = b >= 0;
+            if (pair) q.sp--;
+            if (st && sub == 0) st->c[RT_STAT_ANY_VOL] += pair ? 8 : 4;
+            QChild ca, cb;
+            quad_child2(S, q.cur, b, pair, sub, q.rb, ca, cb);
+            const int oa = ca.ok ? 1 : 0, ob = cb.ok ? 1 : 0;
+            const int a1 = qdpp<RT_QX1>(oa), a2 = qdpp<RT_QX2>(oa), a3 = qdpp<RT_QX3>(oa);
+            const int b1 = qdpp<RT_QX1>(ob), b2 = qdpp<RT_QX2>(ob), b3 = qdpp<RT_QX3>(ob);
+            const int na = oa + a1 + a2 + a3, nb = ob + b1 + b2 + b3;
+            const int pa = (s_lower(sub, 1) ? a1 : 0) + (s_lower(sub, 2) ? a2 : 0) + (s_lower(sub, 3) ? a3 : 0);
+            const int pb = na + (s_lower(sub, 1) ? b1 : 0) + (s_lower(sub, 2) ? b2 : 0) + (s_lower(sub, 3) ? b3 : 0);
+            const int nv = na + nb;
+            if (q.sp + nv - 1 > QSTK::CAP) return -1;
+            // hit k of the 8 slots (A's children, then B's) goes to stack position sp + k - 1; hit 0 is next
+            if (ca.ok && pa > 0) stk.set_rec(q.sp + pa - 1, (uint32_t)ca.item);
+            if (cb.ok && pb > 0) stk.set_rec(q.sp + pb - 1, (uint32_t)cb.item);
+            if (nv > 0) {
+                q.sp += nv - 1;
+                q.cur = qor(ca.ok && pa == 0 ? ca.item : cb.ok && pb == 0 ? cb.item : 0);
+                continue;
+            }
+            q.cur = 0x7ffffffe;
+            break;
+        }
         if (st && sub == 0) st->c[ANY ? RT_STAT_ANY_VOL : RT_STAT_VOL] += 4;
         const float tmax = ANY ? __builtin_inff() : h.t + h.t * RT_T2_WINDOW;
         const QChild c = quad_child(S, q.cur, sub, q.rb, tmax);
