@@ -437,14 +437,18 @@ __device__ __forceinline__ bool qstate_begin(QState& q, V3 o, V3 d, int sub, Sta
 #define RT_VISIT_DESCEND 2  // inner-node trips a quad_visit call may take in a row before returning
                             // (cfg2, refill 8: 1 / 2 / 4 -> 680 / 725 / 706 Msamples/s)
 #endif
+#ifndef RT_CLOSEST_PAIR
+#define RT_CLOSEST_PAIR 0  // closest-hit walks: an inner trip also takes the stack top's node when it is in the window
+                           // (measured: quad visits -8 %, box tests +11 %, fallbacks 375 -> 468, cfg2 710-722 vs 849-855)
+#endif
 #ifndef RT_ANY_PAIR
 #define RT_ANY_PAIR 1  // occlusion walks: an inner trip also takes the stack top's node (8 boxes per round trip;
                        // cfg2 850-858 vs 834-835 Msamples/s, quad visits -6 %, cfg4 8-way shard 411 -> 402 ms)
 #endif
 // Lane sub's children of two inner nodes (a, and b when pair), both records loaded
-// before either is tested: one memory round trip. Occlusion walks (no window).
+// before either is tested: one memory round trip; box tests within [0, tmax].
 __device__ __forceinline__ void quad_child2(const RtSceneView& S, int a, int b, bool pair, int sub, const RayB& rb,
-                                            QChild& ca, QChild& cb)
+                                            float tmax, QChild& ca, QChild& cb)
 {
     float4_ a0, a1, b0 = float4_{0.0f, 0.0f, 0.0f, 0.0f}, b1 = b0;
     child_record(S, a, sub, a0, a1);
@@ -456,13 +460,13 @@ __device__ __forceinline__ void quad_child2(const RtSceneView& S, int a, int b, 
     {
         const int ref = (int)rt_asuint(a1.z), cnt = (int)rt_asuint(a1.w);
         const float mn[3] = {a0.x, a0.y, a0.z}, mx[3] = {a0.w, a1.x, a1.y};
-        ca.ok = cnt >= 0 && box_hit(mn, mx, rb, __builtin_inff(), ca.tn);
+        ca.ok = cnt >= 0 && box_hit(mn, mx, rb, tmax, ca.tn) && ca.tn <= tmax;
         ca.item = cnt > 0 ? leaf_item(ref, cnt) : ref;
     }
     {
         const int ref = (int)rt_asuint(b1.z), cnt = (int)rt_asuint(b1.w);
         const float mn[3] = {b0.x, b0.y, b0.z}, mx[3] = {b0.w, b1.x, b1.y};
-        cb.ok = pair && cnt >= 0 && box_hit(mn, mx, rb, __builtin_inff(), cb.tn);
+        cb.ok = pair && cnt >= 0 && box_hit(mn, mx, rb, tmax, cb.tn) && cb.tn <= tmax;
         cb.item = cnt > 0 ? leaf_item(ref, cnt) : ref;
     }
 }
@@ -482,7 +486,7 @@ __device__ __forceinline__ int quad_visit(const RtSceneView& S, QState& q, QSTK&
             if (pair) q.sp--;
             if (st && sub == 0) st->c[RT_STAT_ANY_VOL] += pair ? 8 : 4;
             QChild ca, cb;
-            quad_child2(S, q.cur, b, pair, sub, q.rb, ca, cb);
+            quad_child2(S, q.cur, b, pair, sub, q.rb, __builtin_inff(), ca, cb);
             const int oa = ca.ok ? 1 : 0, ob = cb.ok ? 1 : 0;
             const int a1 = qdpp<RT_QX1>(oa), a2 = qdpp<RT_QX2>(oa), a3 = qdpp<RT_QX3>(oa);
             const int b1 = qdpp<RT_QX1>(ob), b2 = qdpp<RT_QX2>(ob), b3 = qdpp<RT_QX3>(ob);
@@ -497,6 +501,43 @@ __device__ __forceinline__ int quad_visit(const RtSceneView& S, QState& q, QSTK&
             if (nv > 0) {
                 q.sp += nv - 1;
                 q.cur = qor(ca.ok && pa == 0 ? ca.item : cb.ok && pb == 0 ? cb.item : 0);
+                continue;
+            }
+            q.cur = 0x7ffffffe;
+            break;
+        }
+        if (!ANY && RT_CLOSEST_PAIR) {
+            // the stack top (the nearest pending box), when it is an inner node within the
+            // window, is walked in the same trip; the 8 children are ranked together
+            const float tmax = h.t + h.t * RT_T2_WINDOW;
+            int b = -1;
+            if (q.sp > 0) {
+                const int t = (int)stk.rec(q.sp - 1);
+                if (t >= 0 && stk.key(q.sp - 1) <= tmax) b = t;
+            }
+            const bool pair = b >= 0;
+            if (pair) q.sp--;
+            if (st && sub == 0) st->c[RT_STAT_VOL] += pair ? 8 : 4;
+            QChild ca, cb;
+            quad_child2(S, q.cur, b, pair, sub, q.rb, tmax, ca, cb);
+            const float ka = ca.ok ? ca.tn : __builtin_inff(), kb = cb.ok ? cb.tn : __builtin_inff();
+            const float a1 = qdppf<RT_QX1>(ka), a2 = qdppf<RT_QX2>(ka), a3 = qdppf<RT_QX3>(ka);
+            const float b1 = qdppf<RT_QX1>(kb), b2 = qdppf<RT_QX2>(kb), b3 = qdppf<RT_QX3>(kb);
+            const int s1 = sub ^ 1, s2 = sub ^ 2, s3 = sub ^ 3;
+            // slots: A's children sub 0-3, then B's 4-7; ties go to the lower slot
+            const int ra = (a1 < ka || (a1 == ka && s1 < sub) ? 1 : 0) + (a2 < ka || (a2 == ka && s2 < sub) ? 1 : 0) +
+                           (a3 < ka || (a3 == ka && s3 < sub) ? 1 : 0) + (kb < ka ? 1 : 0) + (b1 < ka ? 1 : 0) +
+                           (b2 < ka ? 1 : 0) + (b3 < ka ? 1 : 0);
+            const int rb = (b1 < kb || (b1 == kb && s1 < sub) ? 1 : 0) + (b2 < kb || (b2 == kb && s2 < sub) ? 1 : 0) +
+                           (b3 < kb || (b3 == kb && s3 < sub) ? 1 : 0) + (ka <= kb ? 1 : 0) + (a1 <= kb ? 1 : 0) +
+                           (a2 <= kb ? 1 : 0) + (a3 <= kb ? 1 : 0);
+            const int nv = qsum((ca.ok ? 1 : 0) + (cb.ok ? 1 : 0));
+            if (q.sp + nv - 1 > QSTK::CAP) return -1;
+            if (ca.ok && ra > 0) stk.set(q.sp + nv - 1 - ra, (uint32_t)ca.item, ka);
+            if (cb.ok && rb > 0) stk.set(q.sp + nv - 1 - rb, (uint32_t)cb.item, kb);
+            if (nv > 0) {
+                q.sp += nv - 1;
+                q.cur = qor(ca.ok && ra == 0 ? ca.item : cb.ok && rb == 0 ? cb.item : 0);
                 continue;
             }
             q.cur = 0x7ffffffe;
