@@ -441,6 +441,10 @@ __device__ __forceinline__ bool qstate_begin(QState& q, V3 o, V3 d, int sub, Sta
 #define RT_CLOSEST_PAIR 0  // closest-hit walks: an inner trip also takes the stack top's node when it is in the window
                            // (measured: quad visits -8 %, box tests +11 %, fallbacks 375 -> 468, cfg2 710-722 vs 849-855)
 #endif
+#ifndef RT_ANY_WIDE
+#define RT_ANY_WIDE 2  // nodes per occlusion trip with RT_ANY_PAIR (2: the current one and the stack top;
+                       // 3 measured 821-824 vs 848-853 Msamples/s on cfg2)
+#endif
 #ifndef RT_ANY_PAIR
 #define RT_ANY_PAIR 1  // occlusion walks: an inner trip also takes the stack top's node (8 boxes per round trip;
                        // cfg2 850-858 vs 834-835 Msamples/s, quad visits -6 %, cfg4 8-way shard 411 -> 402 ms)
@@ -478,29 +482,64 @@ __device__ __forceinline__ int quad_visit(const RtSceneView& S, QState& q, QSTK&
 #pragma unroll 1
     for (int dd = 0; dd < DESC && q.cur >= 0; dd++) {
         if (ANY && RT_ANY_PAIR) {
-            // the stack top, when it is an inner node, is walked in the same trip (the
-            // occlusion answer does not depend on the visit order)
-            int b = -1;
-            if (q.sp > q.bot) b = (int)stk.rec(q.sp - 1);
-            const bool pair = b >= 0;
-            if (pair) q.sp--;
-            if (st && sub == 0) st->c[RT_STAT_ANY_VOL] += pair ? 8 : 4;
-            QChild ca, cb;
-            quad_child2(S, q.cur, b, pair, sub, q.rb, __builtin_inff(), ca, cb);
-            const int oa = ca.ok ? 1 : 0, ob = cb.ok ? 1 : 0;
-            const int a1 = qdpp<RT_QX1>(oa), a2 = qdpp<RT_QX2>(oa), a3 = qdpp<RT_QX3>(oa);
-            const int b1 = qdpp<RT_QX1>(ob), b2 = qdpp<RT_QX2>(ob), b3 = qdpp<RT_QX3>(ob);
-            const int na = oa + a1 + a2 + a3, nb = ob + b1 + b2 + b3;
-            const int pa = (s_lower(sub, 1) ? a1 : 0) + (s_lower(sub, 2) ? a2 : 0) + (s_lower(sub, 3) ? a3 : 0);
-            const int pb = na + (s_lower(sub, 1) ? b1 : 0) + (s_lower(sub, 2) ? b2 : 0) + (s_lower(sub, 3) ? b3 : 0);
-            const int nv = na + nb;
+            // the stack top (RT_ANY_WIDE 3: the top two) inner nodes are walked in the same
+            // trip (the occlusion answer does not depend on the visit order)
+            constexpr int NW = RT_ANY_WIDE;
+            int nd[NW];
+            nd[0] = q.cur;
+            int m = 1;
+#pragma unroll
+            for (int j = 1; j < NW; j++) {
+                nd[j] = -1;
+                if (m == j && q.sp > q.bot) {
+                    const int t = (int)stk.rec(q.sp - 1);
+                    if (t >= 0) {
+                        nd[j] = t;
+                        q.sp--;
+                        m++;
+                    }
+                }
+            }
+            if (st && sub == 0) st->c[RT_STAT_ANY_VOL] += 4 * m;
+            float4_ r0[NW], r1[NW];
+#pragma unroll
+            for (int j = 0; j < NW; j++) {
+                r0[j] = r1[j] = float4_{0.0f, 0.0f, 0.0f, 0.0f};
+                if (j < m) child_record(S, nd[j], sub, r0[j], r1[j]);
+            }
+#pragma unroll
+            for (int j = 0; j < NW; j++) {
+                rt_pin(r0[j]);
+                rt_pin(r1[j]);
+            }
+            int base = 0, first = 0;
+            bool any_first = false;
+#pragma unroll
+            for (int j = 0; j < NW; j++) {
+                const int ref = (int)rt_asuint(r1[j].z), cnt = (int)rt_asuint(r1[j].w);
+                const float mn[3] = {r0[j].x, r0[j].y, r0[j].z}, mx[3] = {r0[j].w, r1[j].x, r1[j].y};
+                float tn;
+                const bool ok = j < m && cnt >= 0 && box_hit(mn, mx, q.rb, __builtin_inff(), tn);
+                const int item = cnt > 0 ? leaf_item(ref, cnt) : ref;
+                const int o = ok ? 1 : 0;
+                const int o1 = qdpp<RT_QX1>(o), o2 = qdpp<RT_QX2>(o), o3 = qdpp<RT_QX3>(o);
+                const int pre = base + (s_lower(sub, 1) ? o1 : 0) + (s_lower(sub, 2) ? o2 : 0) + (s_lower(sub, 3) ? o3 : 0);
+                // hit k of the 4 * NW slots (node 0's children, then node 1's, ...) goes to
+                // stack position sp + k - 1; hit 0 is next
+                if (ok && pre > 0) {
+                    if (q.sp + pre - 1 < QSTK::CAP) stk.set_rec(q.sp + pre - 1, (uint32_t)item);
+                }
+                if (ok && pre == 0) {
+                    first = item;
+                    any_first = true;
+                }
+                base += o + o1 + o2 + o3;
+            }
+            const int nv = base;
             if (q.sp + nv - 1 > QSTK::CAP) return -1;
-            // hit k of the 8 slots (A's children, then B's) goes to stack position sp + k - 1; hit 0 is next
-            if (ca.ok && pa > 0) stk.set_rec(q.sp + pa - 1, (uint32_t)ca.item);
-            if (cb.ok && pb > 0) stk.set_rec(q.sp + pb - 1, (uint32_t)cb.item);
             if (nv > 0) {
                 q.sp += nv - 1;
-                q.cur = qor(ca.ok && pa == 0 ? ca.item : cb.ok && pb == 0 ? cb.item : 0);
+                q.cur = qor(any_first ? first : 0);
                 continue;
             }
             q.cur = 0x7ffffffe;
