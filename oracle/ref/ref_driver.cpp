@@ -163,7 +163,7 @@ int main(int argc, char** argv)
         std::fprintf(stderr,
                      "usage:\n  ref_driver parse <obj> <out>\n  ref_driver bvh <obj> <out>\n"
                      "  ref_driver bvhtests <obj> <out>\n  ref_driver rays <obj> <rays> <out>\n"
-                     "  ref_driver camera <name> <out>\n  ref_driver cdf <env> <out>\n"
+                     "  ref_driver brute <obj> <rays> <out>\n  ref_driver camera <name> <out>\n  ref_driver cdf <env> <out>\n"
                      "  ref_driver render <obj> <env> <camera> W H spp bounces <out>\n"
                      "  ref_driver pixels <obj> <env> <camera> W H spp bounces <pixels> <out>\n");
         return 2;
@@ -254,6 +254,35 @@ int main(int argc, char** argv)
             Ray r(Point(rv[i * 6 + 0], rv[i * 6 + 1], rv[i * 6 + 2]),
                   Vector(rv[i * 6 + 3], rv[i * 6 + 4], rv[i * 6 + 5]));
             found[i] = bvh.intersect(r, hits[i]) ? 1 : 0;
+        }
+        Out o(argv[4]);
+        o.i32(n);
+        for (int i = 0; i < n; i++) write_hit(o, found[i], hits[i]);
+        return 0;
+    }
+    if (cmd == "brute") {
+        // RenderKernel::intersect_scene (render_kernel.h:65, render_kernel.cpp:453-483): the
+        // brute-force triangle loop + sphere loop, public and compiled in every build, on a
+        // ray list; spheres (RT_SPHERES) as main.cpp:74 adds them.
+        Scene s;
+        load_scene(s, argv[2], nullptr);
+        FILE* f = std::fopen(argv[3], "rb");
+        int n;
+        if (!f || std::fread(&n, 4, 1, f) != 1) return 1;
+        std::vector<float> rv((size_t)n * 6);
+        if (std::fread(rv.data(), 4, rv.size(), f) != rv.size()) return 1;
+        std::fclose(f);
+        Image fb(1, 1), sky(1, 1);
+        std::vector<float> cdf(1, 0.0f);
+        RenderKernel rk(1, 1, 1, 1, fb, s.obj.triangles, s.obj.materials, s.obj.emissive_triangle_indices,
+                        s.obj.material_indices, s.spheres, *s.bvh, sky, cdf);
+        std::vector<HitInfo> hits(n);
+        std::vector<int> found(n);
+#pragma omp parallel for schedule(dynamic, 16)
+        for (int i = 0; i < n; i++) {
+            Ray r(Point(rv[i * 6 + 0], rv[i * 6 + 1], rv[i * 6 + 2]),
+                  Vector(rv[i * 6 + 3], rv[i * 6 + 4], rv[i * 6 + 5]));
+            found[i] = rk.intersect_scene(r, hits[i]) ? 1 : 0;
         }
         Out o(argv[4]);
         o.i32(n);

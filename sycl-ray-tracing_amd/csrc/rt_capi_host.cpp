@@ -2,6 +2,7 @@
 // (include/rt_hip.h): argument checking, host scene preparation, host
 // helpers. The compute half lives in rt_render.hip (gfx950).
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 
@@ -10,6 +11,7 @@
 namespace {
 std::mutex g_err_mu;
 std::string g_err;
+thread_local std::string* tl_sink = nullptr;  // rt_err_sink
 void set_global_err(const std::string& m)
 {
     std::lock_guard<std::mutex> lk(g_err_mu);
@@ -17,9 +19,15 @@ void set_global_err(const std::string& m)
 }
 }  // namespace
 
+void rt_err_sink(std::string* sink) { tl_sink = sink; }
+
 int rt_fail(rt_context* ctx, int code, const std::string& msg)
 {
-    if (ctx) {  // (a multi-device render fails from its device threads)
+    if (tl_sink) {  // a device thread of a multi-device render: its own slot (rt_for_devices)
+        *tl_sink = msg;
+        return code;
+    }
+    if (ctx) {
         std::lock_guard<std::mutex> lk(g_err_mu);
         ctx->err = msg;
     }
@@ -107,9 +115,23 @@ int rt_create_multi(int n_devices, const int* devices, rt_context** out)
     if (!out) return rt_fail(nullptr, RT_ERR_ARG, "rt_create_multi: out is NULL");
     *out = nullptr;
     if (n_devices < 1 || n_devices > 64) return rt_fail(nullptr, RT_ERR_ARG, "rt_create_multi: n_devices must be 1..64");
+    // ids: non-negative and distinct (one rank per GPU in the RCCL clique); the range is
+    // checked against the devices present when the backend opens them (RT_ERR_NODEV).
+    // RT_MULTI_LOOPBACK=1 (test knob) admits a list that names a GPU more than once: the
+    // context then exchanges the shards with device copies instead of RCCL, so the
+    // multi-device driver (threads, streams, pack / un-permute) runs on a one-GPU box.
+    const bool loopback = std::getenv("RT_MULTI_LOOPBACK") && std::atoi(std::getenv("RT_MULTI_LOOPBACK")) != 0;
+    for (int d = 0; d < n_devices; d++) {
+        const int id = devices ? devices[d] : d;
+        if (id < 0) return rt_fail(nullptr, RT_ERR_ARG, "rt_create_multi: negative device id");
+        for (int e = 0; e < d; e++)
+            if ((devices ? devices[e] : e) == id && !loopback)
+                return rt_fail(nullptr, RT_ERR_ARG, "rt_create_multi: device " + std::to_string(id) + " listed twice");
+    }
     rt_context* c = new rt_context();
     for (int d = 0; d < n_devices; d++) c->devices.push_back(devices ? devices[d] : d);
     c->device = c->devices[0];
+    c->loopback = loopback;
     int r = rt_backend_create(c);
     if (r) {
         set_global_err(c->err);

@@ -5,7 +5,9 @@
 // suite) implements the rt_backend_* hooks.
 #pragma once
 
+#include <cstdlib>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/rt_hip.h"
@@ -15,8 +17,10 @@
 struct rt_context {
     int device = 0;
     // rt_create_multi: the devices a render shards over (rows y -> device y mod N, RCCL
-    // scatter / gather through devices[0]); empty for a single-device context (rt_create)
+    // scatter / gather through devices[0]); empty for a single-device context (rt_create).
+    // One entry: a single-device context on that ordinal (nothing to shard, no RCCL)
     std::vector<int> devices;
+    bool loopback = false;        // devices may repeat: shards exchanged by device copies, not RCCL
     std::string err;
 
     // RenderKernel constructor inputs (render_kernel.h:27-34)
@@ -62,6 +66,37 @@ int rt_backend_render_pixels(rt_context* ctx, int w, int h, int spp, int bounces
 int rt_backend_intersect(rt_context* ctx, const float* rays, int n, void* out);
 
 int rt_fail(rt_context* ctx, int code, const std::string& msg);
+// While set (per host thread), rt_fail writes its message to *sink instead of the
+// context: the per-device threads of a multi-device render report into their own
+// slots, and the caller raises the error once, after the join (rt_for_devices).
+void rt_err_sink(std::string* sink);
+
+// fn(d) for every device d of a multi-device render: d >= 1 on threads of their own,
+// d = 0 on the caller's. Each device's errors go to its own slot; after the join the
+// lowest failing device's code and message are raised on the context (one writer).
+// RT_FAIL_DEVICE=d (test knob) fails device d before its work starts.
+template <class F>
+int rt_for_devices(rt_context* c, int n, F fn)
+{
+    std::vector<int> rc(n, 0);
+    std::vector<std::string> msg(n);
+    int inject = -1;
+    if (const char* e = std::getenv("RT_FAIL_DEVICE")) inject = std::atoi(e);
+    auto one = [&](int d) {
+        rt_err_sink(&msg[d]);
+        rc[d] = d == inject ? rt_fail(c, RT_ERR_STATE, "injected failure (RT_FAIL_DEVICE)") : fn(d);
+        rt_err_sink(nullptr);
+    };
+    {
+        std::vector<std::thread> th;
+        for (int d = 1; d < n; d++) th.emplace_back(one, d);
+        one(0);
+        for (auto& t : th) t.join();
+    }
+    for (int d = 0; d < n; d++)
+        if (rc[d]) return rt_fail(c, rc[d], "device " + std::to_string(d) + ": " + msg[d]);
+    return 0;
+}
 RtSceneView rt_host_view(const rt_context* ctx);  // host-memory view (hostsim)
 // Does any primitive (triangle or sphere) use a material with a positive
 // emission component (the test at render_kernel.cpp:696)? If not, the

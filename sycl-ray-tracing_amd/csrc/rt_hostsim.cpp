@@ -31,11 +31,11 @@ int rt_backend_create(rt_context*) { return RT_OK; }
 void rt_backend_destroy(rt_context*) {}
 int rt_backend_upload(rt_context*) { return RT_OK; }
 
-static void merge_stats(rt_context* c, const std::vector<rtk::Stats>& s)
+static void merge_stats(unsigned long long* out, const std::vector<rtk::Stats>& s)
 {
-    for (int i = 0; i < RT_STAT_COUNT; i++) c->stats[i] = 0;
+    for (int i = 0; i < RT_STAT_COUNT; i++) out[i] = 0;
     for (const auto& t : s)
-        for (int i = 0; i < RT_STAT_COUNT; i++) c->stats[i] += t.c[i];
+        for (int i = 0; i < RT_STAT_COUNT; i++) out[i] += t.c[i];
 }
 
 // The product's wavefront loop (rt_render.hip run_wave) on the host:
@@ -48,7 +48,7 @@ static void host_append(const rtk::WaveView& W, int32_t* act_count, int p, const
 }
 
 static int run_wave_host(rt_context* c, int w, int h, int spp, int bounces, const rtk::PixSrc& src, int n,
-                         float4_* fb)
+                         float4_* fb, unsigned long long* stats_out)
 {
     if (n <= 0) return RT_OK;
     rtk::WaveView W{};
@@ -233,7 +233,7 @@ static int run_wave_host(rt_context* c, int w, int h, int spp, int bounces, cons
     }
 #pragma omp parallel for schedule(static)
     for (int p = 0; p < n; p++) rtk::tonemap_pixel(W, p);
-    merge_stats(c, st);
+    merge_stats(stats_out, st);
     return RT_OK;
 }
 
@@ -248,20 +248,24 @@ static int render_shard(rt_context* c, int w, int h, int spp, int bounces, int o
     const int N = c->devices.empty() ? 1 : (int)c->devices.size();
     if (N == 1) {
         rtk::PixSrc src{w, off, stride, nullptr};
-        return run_wave_host(c, w, h, spp, bounces, src, rows * w, shard);
+        return run_wave_host(c, w, h, spp, bounces, src, rows * w, shard, c->stats);
     }
-    std::vector<rtk::Stats> sum(1);
-    std::memset(&sum[0], 0, sizeof sum[0]);
-    for (int d = 0; d < N; d++) {
+    // one host thread per "device", as render_multi (rt_for_devices: per-device error slots)
+    std::vector<std::vector<unsigned long long>> dst(N, std::vector<unsigned long long>(RT_STAT_COUNT, 0));
+    const int r = rt_for_devices(c, N, [&](int d) {
         const int rows_d = rows > d ? (rows - d + N - 1) / N : 0;
         std::vector<float4_> blk((size_t)rows_d * w);
         for (int k = 0; k < rows_d; k++) std::memcpy(&blk[(size_t)k * w], shard + (size_t)(d + k * N) * w, 16 * (size_t)w);
         rtk::PixSrc src{w, off + d * stride, N * stride, nullptr};
-        if (int r = run_wave_host(c, w, h, spp, bounces, src, rows_d * w, blk.data())) return r;
+        if (int e = run_wave_host(c, w, h, spp, bounces, src, rows_d * w, blk.data(), dst[d].data())) return e;
         for (int k = 0; k < rows_d; k++) std::memcpy(shard + (size_t)(d + k * N) * w, &blk[(size_t)k * w], 16 * (size_t)w);
-        for (int i = 0; i < RT_STAT_COUNT; i++) sum[0].c[i] += rows_d ? c->stats[i] : 0;
+        return 0;
+    });
+    if (r) return r;
+    for (int i = 0; i < RT_STAT_COUNT; i++) {
+        c->stats[i] = 0;
+        for (int d = 0; d < N; d++) c->stats[i] += dst[d][i];
     }
-    merge_stats(c, sum);
     return RT_OK;
 }
 
@@ -292,7 +296,7 @@ int rt_backend_render(rt_context* c, int w, int h, int spp, int bounces, float* 
 int rt_backend_render_pixels(rt_context* c, int w, int h, int spp, int bounces, const int* xy, int n, float* rgba)
 {
     rtk::PixSrc src{w, 0, 1, xy};
-    return run_wave_host(c, w, h, spp, bounces, src, n, (float4_*)rgba);
+    return run_wave_host(c, w, h, spp, bounces, src, n, (float4_*)rgba, c->stats);
 }
 
 int rt_backend_intersect(rt_context* c, const float* rays, int n, void* out)
@@ -328,7 +332,7 @@ int rt_backend_intersect(rt_context* c, const float* rays, int n, void* out)
             std::memcpy(o + 10, &neg1, 4);
         }
     }
-    merge_stats(c, st);
+    merge_stats(c->stats, st);
     return RT_OK;
 }
 

@@ -1440,8 +1440,9 @@ namespace {
 // framebuffer; a render shards its rows over the devices (render_multi).
 struct Group {
     std::vector<Backend*> dev;     // dev[0]: the root
-    bool multi = false;            // rt_create_multi (even with one device: the RCCL path)
-    std::vector<ncclComm_t> comms; // ncclCommInitAll over the devices, in order
+    bool multi = false;            // rt_create_multi over two or more devices
+    bool loopback = false;         // (RT_MULTI_LOOPBACK test contexts) shards exchanged by device copies
+    std::vector<ncclComm_t> comms; // ncclCommInitAll over the devices, in order (RCCL exchange)
     DevBuf stage;                  // root: N blocks of rows_max rows (scatter source / gather target)
     std::vector<DevBuf> shard;     // device d >= 1: its block
 };
@@ -1558,6 +1559,9 @@ void destroy_one(Backend* b)
 int upload_one(rt_context* c, Backend* b, const std::vector<int32_t>& matk, bool mats_only)
 {
     HIPCHK(c, hipSetDevice(b->device));
+    // the previous render may still run (rt_render_device returns at once, its kernels on
+    // non-blocking streams that a null-stream copy does not wait for): it reads these tables
+    if (b->done_recorded) HIPCHK(c, hipEventSynchronize(b->ev_done));
     int r = 0;
     if (mats_only) {  // rt_set_materials: the material table (and what depends on it) alone
         if ((r = upload(c, b->mats, c->mats))) return r;
@@ -1625,7 +1629,8 @@ int rt_backend_create(rt_context* c)
 {
     Group* g = new Group();
     c->backend = g;
-    g->multi = !c->devices.empty();
+    g->multi = c->devices.size() > 1;  // (one listed device: a single-device context on it)
+    g->loopback = g->multi && c->loopback;
     const std::vector<int> ids = g->multi ? c->devices : std::vector<int>{c->device};
     for (int d : ids) {
         Backend* b = nullptr;
@@ -1633,13 +1638,13 @@ int rt_backend_create(rt_context* c)
         if (b) g->dev.push_back(b);
         if (r) return r;
     }
-    if (g->multi) {
+    if (g->multi) g->shard.resize(ids.size());
+    if (g->multi && !g->loopback) {
         std::string err;
         const Rccl* R = rccl_load(err);
         if (!R) return rt_fail(c, RT_ERR_NODEV, err);
         g->comms.resize(ids.size());
         NCCLCHK(c, R, R->init(g->comms.data(), (int)ids.size(), ids.data()));
-        g->shard.resize(ids.size());
     }
     return RT_OK;
 }
@@ -2013,8 +2018,8 @@ int render_multi(rt_context* c, Group* g, int w, int h, int spp, int bounces, fl
 {
     const int N = (int)g->dev.size();
     std::string err;
-    const Rccl* R = rccl_load(err);
-    if (!R) return rt_fail(c, RT_ERR_NODEV, err);
+    const Rccl* R = nullptr;
+    if (!g->loopback && !(R = rccl_load(err))) return rt_fail(c, RT_ERR_NODEV, err);
     const int rows = (h - off + stride - 1) / stride;
     const int rows_max = (rows + N - 1) / N;
     const size_t blk = (size_t)rows_max * w;  // float4 per block
@@ -2036,39 +2041,47 @@ int render_multi(rt_context* c, Group* g, int w, int h, int spp, int bounces, fl
     std::vector<hipStream_t> st(N);
     for (int d = 0; d < N; d++) st[d] = d == 0 ? s : g->dev[d]->own;
     const size_t cnt = blk * 4;  // floats per block
-    NCCLCHK(c, R, R->group_start());
-    for (int d = 0; d < N; d++)
-        NCCLCHK(c, R, R->scatter(stage, d == 0 ? (void*)stage : g->shard[d].p, cnt, ncclFloat, 0, g->comms[d], st[d]));
-    NCCLCHK(c, R, R->group_end());
-    // the wavefront loops, one host thread per device
-    std::vector<int> rc(N, RT_OK);
-    auto work = [&](int d) {
-        Backend* b = g->dev[d];
-        if (hipSetDevice(b->device) != hipSuccess) {
-            rc[d] = rt_fail(c, RT_ERR_HIP, "render: hipSetDevice failed");
-            return;
+    if (g->loopback) {  // block d -> device d by a device copy on the root stream; the shard streams wait for it
+        for (int d = 1; d < N; d++)
+            HIPCHK(c, hipMemcpyAsync(g->shard[d].p, stage + d * blk, blk * sizeof(float4_), hipMemcpyDeviceToDevice, s));
+        HIPCHK(c, hipEventRecord(root->ev_fork, s));
+        for (int d = 1; d < N; d++) {
+            HIPCHK(c, hipSetDevice(g->dev[d]->device));
+            HIPCHK(c, hipStreamWaitEvent(st[d], root->ev_fork, 0));
         }
-        if (c->stats_enabled && hipMemsetAsync(b->stats.p, 0, b->stats.bytes, st[d]) != hipSuccess) {
-            rc[d] = rt_fail(c, RT_ERR_HIP, "render: stats reset failed");
-            return;
-        }
-        const rtk::PixSrc src{w, off + d * stride, N * stride, nullptr};
-        float4_* dst = d == 0 ? stage : (float4_*)g->shard[d].p;
-        rc[d] = run_wave(c, b, w, h, spp, bounces, src, rows_of(d) * w, dst, st[d]);
-    };
-    {
-        std::vector<std::thread> th;
-        for (int d = 1; d < N; d++) th.emplace_back(work, d);
-        work(0);
-        for (auto& t : th) t.join();
+        HIPCHK(c, hipSetDevice(root->device));
+    } else {
+        NCCLCHK(c, R, R->group_start());
+        for (int d = 0; d < N; d++)
+            NCCLCHK(c, R, R->scatter(stage, d == 0 ? (void*)stage : g->shard[d].p, cnt, ncclFloat, 0, g->comms[d], st[d]));
+        NCCLCHK(c, R, R->group_end());
     }
-    for (int d = 0; d < N; d++)
-        if (rc[d]) return rc[d];
+    // the wavefront loops, one host thread per device; errors are collected per device
+    // and raised once after the join (rt_for_devices). run_wave resets the stats itself.
+    if (int r = rt_for_devices(c, N, [&](int d) -> int {
+            Backend* b = g->dev[d];
+            HIPCHK(c, hipSetDevice(b->device));
+            const rtk::PixSrc src{w, off + d * stride, N * stride, nullptr};
+            float4_* dst = d == 0 ? stage : (float4_*)g->shard[d].p;
+            return run_wave(c, b, w, h, spp, bounces, src, rows_of(d) * w, dst, st[d]);
+        }))
+        return r;
     HIPCHK(c, hipSetDevice(root->device));
-    NCCLCHK(c, R, R->group_start());
-    for (int d = 0; d < N; d++)
-        NCCLCHK(c, R, R->gather(d == 0 ? (const void*)stage : g->shard[d].p, stage, cnt, ncclFloat, 0, g->comms[d], st[d]));
-    NCCLCHK(c, R, R->group_end());
+    if (g->loopback) {  // each block back to the root after its device's loop; the root stream waits for all
+        for (int d = 1; d < N; d++) {
+            Backend* b = g->dev[d];
+            HIPCHK(c, hipSetDevice(b->device));
+            HIPCHK(c, hipMemcpyAsync(stage + d * blk, g->shard[d].p, blk * sizeof(float4_), hipMemcpyDeviceToDevice, st[d]));
+            HIPCHK(c, hipEventRecord(b->ev_join[0], st[d]));
+            HIPCHK(c, hipSetDevice(root->device));
+            HIPCHK(c, hipStreamWaitEvent(s, b->ev_join[0], 0));
+        }
+    } else {
+        NCCLCHK(c, R, R->group_start());
+        for (int d = 0; d < N; d++)
+            NCCLCHK(c, R, R->gather(d == 0 ? (const void*)stage : g->shard[d].p, stage, cnt, ncclFloat, 0, g->comms[d], st[d]));
+        NCCLCHK(c, R, R->group_end());
+    }
     for (int d = 0; d < N; d++)
         if (rows_of(d))
             HIPCHK(c, hipMemcpy2DAsync(fb + (size_t)d * w, N * pitch, stage + d * blk, pitch, pitch, rows_of(d),

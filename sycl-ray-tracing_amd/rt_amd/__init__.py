@@ -24,7 +24,8 @@ from dataclasses import dataclass, field
 
 import numpy as np
 
-from ._capi import RtError, check, lib, ptr
+from ._capi import (RT_ERR_ARG, RT_ERR_HIP, RT_ERR_IO, RT_ERR_NODEV, RT_ERR_STATE, RT_OK,  # noqa: F401
+                    RtError, check, lib, ptr)
 
 __all__ = ["Camera", "Image", "ParsedOBJ", "parse_obj", "compute_env_map_cdf", "luminance_of_pixels", "BVH",
            "RenderKernel", "RtError", "octree_dump", "make_materials", "read_image_float", "write_image_png",

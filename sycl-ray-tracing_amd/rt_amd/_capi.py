@@ -26,6 +26,9 @@ EXPORTS = [
     "rt_set_intersect_mode", "rt_create_multi", "rt_device_count", "rt_set_materials",
 ]
 
+# return codes (include/rt_hip.h)
+RT_OK, RT_ERR_ARG, RT_ERR_HIP, RT_ERR_STATE, RT_ERR_IO, RT_ERR_NODEV = 0, -1, -2, -3, -4, -5
+
 P = ctypes.c_void_p
 I = ctypes.c_int
 L = ctypes.c_long

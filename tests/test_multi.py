@@ -3,11 +3,14 @@ RCCL scatter / gather through the root, include/rt_hip.h) and the material
 table pushed alone (rt_set_materials, the reference's by-reference
 `std::vector<SimpleMaterial>&`, render_kernel.h:81-93).
 
-CPU: the hostsim build shards the same way (host copies in place of RCCL), so
-the row mapping is checked here against the reference's goldens. GPU: the
-product's RCCL path (a one-device clique on a one-GPU box, a two-rank clique
-on one device where RCCL allows it) and the cfg5 material sweep through one
-context, against the compiled reference's goldens."""
+CPU: the hostsim build shards the same way (one host thread per device, host
+copies in place of RCCL), so the row mapping, the per-device error collection
+and recovery are checked here against the reference's goldens. GPU: the
+multi-device driver on one GPU through its loopback exchange (RT_MULTI_LOOPBACK:
+device copies in place of RCCL, which needs distinct GPUs) and the cfg5 material
+sweep through one context, against the compiled reference's goldens. The RCCL
+scatter / gather itself runs only on a node with two or more GPUs (bench.py
+--gpus N, the driver's scaling runs)."""
 from __future__ import annotations
 
 import numpy as np
@@ -46,6 +49,42 @@ def test_hostsim_multi_device_shard_matches_golden(n, off, stride, manifest, cam
     np.testing.assert_array_equal(_bits(shard), _bits(e["expected"][off::stride]))
 
 
+@pytest.mark.parametrize("bad", [1, 2])
+def test_hostsim_multi_device_failure_surfaces_and_recovers(bad, manifest, cameras, monkeypatch):
+    """A device >= 1 failing inside a multi-device render (RT_FAIL_DEVICE test knob):
+    the render returns its error code with the device's message (collected in the
+    device thread's own slot, raised once after the join), and the next render on
+    the same context succeeds bit for bit."""
+    e = rt_cases.golden_case("cornell32_128", manifest)
+    rk, fb = rt_cases.make_kernel(e, cameras, hostsim=True, device=[0, 1, 2])
+    monkeypatch.setenv("RT_FAIL_DEVICE", str(bad))
+    with pytest.raises(rt_amd.RtError) as ei:
+        rk.render()
+    assert f"({rt_amd.RT_ERR_STATE})" in str(ei.value) and f"device {bad}: injected failure" in str(ei.value)
+    monkeypatch.delenv("RT_FAIL_DEVICE")
+    fb.pixels[...] = rt_amd.Image(e["W"], e["H"]).pixels
+    rk.render()
+    np.testing.assert_array_equal(_bits(fb.pixels), _bits(e["expected"]))
+
+
+def test_create_multi_device_ids(monkeypatch):
+    """rt_create_multi: a device listed twice or a negative id is RT_ERR_ARG; one listed
+    device is a single-device context on that ordinal (nothing to shard, no RCCL)."""
+    import ctypes
+    from rt_amd._capi import lib
+    L = lib(hostsim=True)
+    h = ctypes.c_void_p()
+    monkeypatch.delenv("RT_MULTI_LOOPBACK", raising=False)
+    for ids in ([0, 0], [1, 2, 1], [-1, 0]):
+        a = np.asarray(ids, np.int32)
+        assert L.rt_create_multi(len(ids), a.ctypes.data_as(ctypes.c_void_p), ctypes.byref(h)) == rt_amd.RT_ERR_ARG
+        assert not h.value
+    a = np.asarray([3], np.int32)
+    assert L.rt_create_multi(1, a.ctypes.data_as(ctypes.c_void_p), ctypes.byref(h)) == 0
+    assert L.rt_device_count(h) == 1
+    L.rt_destroy(h)
+
+
 def test_hostsim_materials_edited_in_place(manifest, cameras):
     """Editing the bound material array between renders changes the next
     render exactly as a fresh kernel with the new table would."""
@@ -74,10 +113,9 @@ def test_set_materials_rejects_short_table(manifest, cameras):
 
 # ------------------------------------------------------------------ GPU
 @pytest.mark.gpu
-def test_gpu_multi_context_one_device_matches_single(manifest, cameras):
-    """The RCCL path (pack, ncclScatter, render, ncclGather, un-permute) on a
-    one-device clique: frames and row shards bit-identical to the goldens and
-    to the single-device context."""
+def test_gpu_multi_context_one_device_is_single(manifest, cameras):
+    """device=[0]: one listed device is a single-device context on it (no RCCL);
+    frames and row shards bit-identical to the goldens."""
     from hip_mem import DeviceBuffer
     e = rt_cases.golden_case("cornell32_128", manifest)
     rk, fb = rt_cases.make_kernel(e, cameras, hostsim=False, device=[0])
@@ -93,24 +131,55 @@ def test_gpu_multi_context_one_device_matches_single(manifest, cameras):
         rk.render_device(buf.ptr, off, stride, None)
         got = buf.download(init.shape, np.float32)
         np.testing.assert_array_equal(_bits(got), _bits(e["expected"][off::stride]))
-    g = rt_cases.golden_case("cfg2_dragon", manifest)
-    rk, fb = rt_cases.make_kernel(g, cameras, hostsim=False, device=[0])
-    rk.ray_trace_pixels(g["px"])
-    got = fb.pixels[g["px"][:, 1], g["px"][:, 0]]
-    assert gio.compare_rgb(got, g["expected"])["bitwise_fraction"] == 1.0
 
 
 @pytest.mark.gpu
-def test_gpu_multi_context_two_ranks_one_device(manifest, cameras):
-    """A two-rank RCCL clique on device 0 twice (skipped where RCCL refuses two
-    ranks on one GPU): the N=2 scatter / gather and un-permute on one box."""
+@pytest.mark.parametrize("ids", [[0, 0], [0, 0, 0]])
+def test_gpu_multi_device_driver_loopback(ids, manifest, cameras, monkeypatch):
+    """The multi-device driver on one GPU (RT_MULTI_LOOPBACK: the device list may name
+    GPU 0 repeatedly; the shards are exchanged with device copies instead of RCCL):
+    the row pack, one host thread and stream per device running its own wavefront
+    loop, the block exchange and the un-permute, bit-identical to the goldens for
+    frames, row shards and the dragon; then a device failure (RT_FAIL_DEVICE) surfaces
+    and the context renders correctly again."""
+    from hip_mem import DeviceBuffer
+    monkeypatch.setenv("RT_MULTI_LOOPBACK", "1")
     e = rt_cases.golden_case("cornell32_128", manifest)
-    try:
-        rk, fb = rt_cases.make_kernel(e, cameras, hostsim=False, device=[0, 0])
-    except rt_amd.RtError as err:
-        pytest.skip(f"RCCL: two ranks on one device refused ({err})")
+    rk, fb = rt_cases.make_kernel(e, cameras, hostsim=False, device=ids)
+    assert rk.n_devices == len(ids)
     rk.render()
     np.testing.assert_array_equal(_bits(fb.pixels), _bits(e["expected"]))
+    for off, stride in ((0, 1), (1, 3)):
+        rows = len(range(off, e["H"], stride))
+        init = np.zeros((rows, e["W"], 4), np.float32)
+        init[..., 3] = 1.0
+        buf = DeviceBuffer(init.nbytes)
+        buf.upload(init)
+        rk.render_device(buf.ptr, off, stride, None)
+        got = buf.download(init.shape, np.float32)
+        np.testing.assert_array_equal(_bits(got), _bits(e["expected"][off::stride]))
+    monkeypatch.setenv("RT_FAIL_DEVICE", str(len(ids) - 1))
+    fb.pixels[...] = rt_amd.Image(e["W"], e["H"]).pixels
+    with pytest.raises(rt_amd.RtError) as ei:
+        rk.render()
+    assert f"device {len(ids) - 1}: injected failure" in str(ei.value)
+    monkeypatch.delenv("RT_FAIL_DEVICE")
+    fb.pixels[...] = rt_amd.Image(e["W"], e["H"]).pixels
+    rk.render()
+    np.testing.assert_array_equal(_bits(fb.pixels), _bits(e["expected"]))
+    # a dragon frame's row shard (cfg2 rows at 4 spp) against the single-device context
+    g = rt_cases.golden_case("cfg2_dragon", manifest)
+    rk2, _ = rt_cases.make_kernel(g, cameras, hostsim=False, device=ids, spp=4)
+    rk1, _ = rt_cases.make_kernel(g, cameras, hostsim=False, device=0, spp=4)
+    outs = []
+    for k in (rk2, rk1):
+        rows = len(range(3, g["H"], 5))
+        init = np.zeros((rows, g["W"], 4), np.float32)
+        buf = DeviceBuffer(init.nbytes)
+        buf.upload(init)
+        k.render_device(buf.ptr, 3, 5, None)
+        outs.append(buf.download(init.shape, np.float32))
+    np.testing.assert_array_equal(_bits(outs[0]), _bits(outs[1]))
 
 
 @pytest.mark.gpu
@@ -131,3 +200,34 @@ def test_gpu_cfg5_sweep_one_context(manifest, cameras):
             got = fb.pixels[e["px"][:, 1], e["px"][:, 0]]
             c = gio.compare_rgb(got, e["expected"])
             assert c["bitwise_fraction"] == 1.0, (m, r, c)
+
+
+@pytest.mark.gpu
+def test_gpu_materials_edit_between_async_renders(manifest, cameras):
+    """render_device returns before its kernels finish (non-blocking lane streams); a
+    material edit pushed right after must not reach the table the running frame reads:
+    render_device, set_materials, render_device with no sync in between, then each
+    frame against a synchronous render of its own table."""
+    from hip_mem import DeviceBuffer
+    g = rt_cases.golden_case("cfg2_dragon", manifest)
+    P = parsed_scene(g["scene"])
+    mats = P.materials.copy()
+    rk, _ = rt_cases.make_kernel(g, cameras, hostsim=False, spp=4, materials=mats)
+    mats2 = mats.copy()
+    mats2[1, 8], mats2[1, 9] = np.float32(1.0), np.float32(0.05)  # the dragon: polished metal
+    H, W = g["H"], g["W"]
+    init = np.zeros((H, W, 4), np.float32)
+    bufs = [DeviceBuffer(init.nbytes), DeviceBuffer(init.nbytes)]
+    for b in bufs:
+        b.upload(init)
+    rk.render_device(bufs[0].ptr, 0, 1, None)
+    mats[...] = mats2  # in place, as the reference's by-reference vector (render_kernel.h:81-93)
+    rk.render_device(bufs[1].ptr, 0, 1, None)
+    got = [b.download(init.shape, np.float32) for b in bufs]
+    for m, frame in ((P.materials, got[0]), (mats2, got[1])):
+        ref, _ = rt_cases.make_kernel(g, cameras, hostsim=False, spp=4, materials=m.copy())
+        b = DeviceBuffer(init.nbytes)
+        b.upload(init)
+        ref.render_device(b.ptr, 0, 1, None)
+        np.testing.assert_array_equal(_bits(frame), _bits(b.download(init.shape, np.float32)))
+    assert not np.array_equal(_bits(got[0]), _bits(got[1]))
