@@ -67,10 +67,25 @@ CONFIGS = {
     # one cfg5 material variant (metalness 1/3, roughness 0.25 on the dragon) at the cfg5 frame
     "cfg5": ("dragon", "L", "dragon", 1920, 1080, 1024, 8,
              "PBRT Dragon stand-in, cfg5 variant m=1/3 r=0.25, 1920x1080x1024spp x8 bounces"),
+    # BASELINE config 5 as replicas: all 16 material variants (metalness x roughness on the dragon,
+    # tools/gen_golden.py), each a 1920x1080x1024spp frame, variant v on GPU v mod N (rt_render_variants)
+    "cfg5sweep": ("dragon", "L", "dragon", 1920, 1080, 1024, 8,
+                  "PBRT Dragon stand-in, Cook-Torrance sweep: 16 material variants (metalness {0,1/3,2/3,1} x "
+                  "roughness {0.05,0.25,0.5,1}) x 1920x1080x1024spp x8 bounces, variant v on GPU v mod N"),
     # profiling-sized cfg2 (same scene / camera / ray mix, 1/16 of the pixels, 1/4 of the samples); not a bench line
     "cfg2s": ("dragon", "L", "dragon", 480, 270, 16, 8, "profiling-sized cfg2: dragon 480x270x16spp x8"),
 }
 CFG5_VARIANT = (1, 1.0 / 3.0, 0.25)  # (material index, metalness, roughness) as tools/gen_golden.py writes them
+CFG5_GRID = [(m, r) for m in range(4) for r in range(4)]  # variant v = (metalness index, roughness index)
+CFG5_METAL = [0.0, 1.0 / 3.0, 2.0 / 3.0, 1.0]
+CFG5_ROUGH = [0.05, 0.25, 0.5, 1.0]
+# The sweep's static schedule: position p of this order renders on GPU p mod N. A variant's
+# frame time follows its roughness (one MI355X, profiles/r03_sweep_variant_ms.json: r = 0.05 /
+# 0.25 / 0.5 / 1.0 -> 2.65 / 2.54 / 2.17 / 1.81 s; metalness within 1.5 %), so the order pairs
+# the slowest with the fastest: N = 8 -> {0.05, 1.0} or {0.25, 0.5} per GPU (max 4.71 s against
+# the 4.58 s mean), N = 4 and 2 -> every roughness on every GPU. (v mod N in grid order would put
+# two r = 0.05 frames on GPU 0: 5.31 s, 0.86.)
+CFG5_ORDER = [0, 4, 8, 12, 1, 5, 9, 13, 3, 7, 11, 15, 2, 6, 10, 14]
 HBM_PEAK_GBS = 8000.0  # /opt/skills/guides/MI355X_MICROARCH.md (spec)
 # Algorithmic bytes per unit of work: the records a query
 # must read. Search-BVH box test 32 B (one child record), triangle test
@@ -140,6 +155,17 @@ def frame_dims(cfg: str, n: int, scaling: str):
         return W, H
     s = math.sqrt(n)
     return int(round(W * s)), int(round(H * s))
+
+
+def cfg5_tables(P):
+    """The 16 cfg5 material tables (material 1 = the dragon's, as tools/gen_golden.py overrides it)."""
+    out = []
+    for mi, ri in CFG5_GRID:
+        m = P.materials.copy()
+        m[1, 8] = np.float32(repr(CFG5_METAL[mi]))
+        m[1, 9] = np.float32(repr(CFG5_ROUGH[ri]))
+        out.append(m)
+    return out
 
 
 def build_inputs(cfg):
@@ -212,6 +238,183 @@ def fail(msg: str, code: int = 2):
     sys.exit(code)
 
 
+def sweep_parity(frames_by_variant, variants) -> dict:
+    """Every golden pixel of the rendered cfg5 variants (tests/golden, written by the compiled
+    reference) against the GPU's frame: per-channel L-inf and the bitwise-identical fraction."""
+    import golden_io as gio
+    got, want = [], []
+    for v, fr in zip(variants, frames_by_variant):
+        mi, ri = CFG5_GRID[v]
+        g = np.load(os.path.join(gio.GOLDEN, f"render_cfg5_sweep_m{mi}_r{ri}.npz"))
+        px = g["px"]
+        got.append(fr[px[:, 1], px[:, 0]])
+        want.append(g["rgba"])
+    c = gio.compare_rgb(np.concatenate(got), np.concatenate(want))
+    c["pixels"] = int(sum(w.shape[0] for w in want))
+    c["against"] = "tests/golden/render_cfg5_sweep_m*_r*.npz (compiled reference, 48 px per variant)"
+    return c
+
+
+def run_sweep(args, rank, world, dev, single_process_multi, torch, dist):
+    """--config cfg5sweep: BASELINE config 5 as replicas. A step renders all 16 material
+    variants (1920x1080x1024spp x8 each); variant v runs on GPU v mod N with no exchange
+    (rt_render_variants: one context over the N GPUs, or under torchrun one context per
+    rank rendering v = rank mod N). Strong scaling: the 16 frames are the whole job.
+    --sim-world K renders only rank 0's share of a K-GPU sweep on this one GPU."""
+    import rt_amd
+    _, _, _, W, H, spp, nb, desc = CONFIGS["cfg5sweep"]
+    n_gpus = args.gpus
+    t0 = time.time()
+    P, sky, cam17 = build_inputs("cfg5sweep")
+    tables = cfg5_tables(P)
+    share = args.sim_world or world
+    # (single process: every variant, position p on GPU p mod N; torchrun / sim: this rank's positions)
+    me = args.sim_rank if args.sim_world else rank
+    mine = [CFG5_ORDER[p] for p in range(len(tables)) if single_process_multi or p % share == me]
+    devices = list(range(n_gpus)) if single_process_multi else dev.index
+    rk = rt_amd.RenderKernel(W, H, spp, nb, rt_amd.Image(1, 1), P.triangles, P.materials,
+                             P.emissive_triangle_indices, P.material_indices, None, rt_amd.BVH(P.triangles),
+                             rt_amd.Image.from_rgb(sky), None, device=devices)
+    rk.set_camera(rt_amd.Camera(cam17[:16], cam17[16]))
+    ndev = n_gpus if single_process_multi else 1
+    init = torch.zeros((H, W, 4), dtype=torch.float32)
+    init[..., 3] = 1.0
+    bufs = [init.to(torch.device("cuda", i % ndev if single_process_multi else dev.index)) for i in range(len(mine))]
+    setup_s = time.time() - t0
+
+    inits = {b.device: init.to(b.device) for b in bufs}
+
+    def step():  # a fresh framebuffer per variant (the reference's Image is read-modify-write), then the sweep
+        for b in bufs:
+            b.copy_(inits[b.device])
+        for d in inits:
+            torch.cuda.synchronize(d)
+        rk.render_variants([tables[v] for v in mine], device_ptrs=[b.data_ptr() for b in bufs])
+
+    for _ in range(args.warmup):
+        step()
+    if world > 1:
+        dist.barrier()
+    t_start = time.perf_counter()
+    kms = []
+    for _ in range(args.steps):
+        step()
+        kms.append(rk.last_kernel_ms())
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t_start
+    cdev = dev if world == 1 or dist.get_backend() == "nccl" else "cpu"  # (gloo rehearsals: host tensors)
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    n_frames = len(tables) if not args.sim_world else len(mine)
+    value = n_frames * W * H * spp * args.steps / elapsed / 1e6
+    frames = [b.cpu().numpy() for b in bufs]
+    parity = sweep_parity(frames, mine)
+    if world > 1:  # parity of every rank's variants, worst case on rank 0
+        pt = torch.tensor([parity["linf"], 1.0 - parity["bitwise_fraction"]], dtype=torch.float64, device=cdev)
+        dist.all_reduce(pt, op=dist.ReduceOp.MAX)
+        parity["linf"], parity["bitwise_fraction"] = float(pt[0]), 1.0 - float(pt[1])
+        parity["pixels"] *= world
+    cpu = None
+    if rank == 0 and world == 1 and n_gpus == 1 and not args.no_cpu_baseline:
+        threads = int(os.environ.get("OMP_NUM_THREADS", 0)) or len(os.sched_getaffinity(0))
+        threads = min(threads, len(os.sched_getaffinity(0)))
+        Pv = rt_amd.parse_obj(__import__("scenes").scene_path("dragon"))
+        Pv.materials = tables[mine[0]]
+        cpu, cpar, _ = cpu_baseline(Pv, sky, cam17, W, H, spp, nb, frames[0], threads, 540)
+        cpu["sample"] = f"variant {mine[0]}: " + cpu["sample"]
+        cpu["parity_rows"] = cpar
+    if rank == 0:
+        if single_process_multi:
+            par = f"one process, rt_render_variants over {n_gpus} GPUs: variant v on GPU v mod {n_gpus}, no exchange"
+        elif world > 1:
+            par = f"{world} processes (torchrun): rank r renders variants v % {world} == r, no exchange"
+        else:
+            par = "1 GPU" + (f" (sim: rank {args.sim_rank}'s share of a {args.sim_world}-GPU sweep)"
+                             if args.sim_world else "")
+        out = {
+            "metric": "Msamples/sec (W×H×spp/s) at 1080p; per-channel L∞ vs CPU ref",
+            "value": round(value, 3), "unit": "Msamples/s", "n_gpus": n_gpus, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
+            "scaling": "strong", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic: procedural 1,000,002-triangle stand-in for the absent pbrt_dragon.obj and a "
+                    "synthetic 2048x1024 env map (SURVEY.md §8d)",
+            "config": {"workload": f"cfg5sweep: {desc}", "W": W, "H": H, "spp": spp, "bounces": nb,
+                       "variants": n_frames, "variants_this_rank": [int(v) for v in mine], "parallelism": par},
+            "setup_s": round(setup_s, 2),
+            "device_ms_per_step": round(float(np.mean(kms)), 2),
+            "roofline": None,  # (the kernels are cfg2's; their roofline is the cfg2 line's: bench.py --config cfg2)
+            "cpu_baseline": cpu,
+            "parity": parity,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def strong_cfg4(args, rk, P, sky, cam17, rank, world, dev, single_process_multi, torch, dist) -> dict:
+    """N > 1: the north star's 8-GPU target config (cfg4: 3840x2160x256spp x8, BASELINE
+    configs[3]) as a STRONG split over the same N GPUs (the line's own partition: rows
+    y % N, RCCL exchange to the root), and the same frame on one GPU alone, one timed
+    render each after a warm-up: efficiency = T_1 / (N * T_N). The line's `value` stays
+    the weak-scaling cfg2 job; this object carries the fixed-size figure."""
+    import rt_amd
+    from rt_amd.dist import ShardedFrame
+    _, _, _, W4, H4, spp4, nb4, desc4 = CONFIGS["cfg4"]
+    n = args.gpus
+    saved = (rk.width, rk.height, rk.render_samples, rk.max_bounces)
+    rk.width, rk.height, rk.render_samples, rk.max_bounces = W4, H4, spp4, nb4
+    stream = torch.cuda.current_stream(dev).cuda_stream
+
+    def timed(frame, gather, reps=1):
+        frame.render(stream)  # warm (and the wave buffers of this size)
+        if gather:
+            frame.gather()
+        torch.cuda.synchronize(dev)
+        if world > 1 and gather:
+            dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            frame.render(stream)
+            if gather:
+                frame.gather()
+        torch.cuda.synchronize(dev)
+        if world > 1 and gather:
+            dist.barrier()
+        return (time.perf_counter() - t0) / reps
+
+    # T_N: the split, exactly as the line's frames are split
+    frame = ShardedFrame(rk, 0, 1, device=dev) if single_process_multi else ShardedFrame(rk, rank, world, device=dev)
+    tn = timed(frame, gather=True)
+    if world > 1:
+        t = torch.tensor([tn], dtype=torch.float64, device=dev if dist.get_backend() == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        tn = float(t.item())
+    del frame
+    rk.width, rk.height, rk.render_samples, rk.max_bounces = saved
+    # T_1: the whole frame on GPU 0 alone (a single-device context; the other ranks wait)
+    t1 = None
+    if rank == 0:
+        k1 = rt_amd.RenderKernel(W4, H4, spp4, nb4, rt_amd.Image(1, 1), P.triangles, P.materials,
+                                 P.emissive_triangle_indices, P.material_indices, None, rt_amd.BVH(P.triangles),
+                                 rt_amd.Image.from_rgb(sky), None, device=dev.index)
+        k1.set_camera(rt_amd.Camera(cam17[:16], cam17[16]))
+        t1 = timed(ShardedFrame(k1, 0, 1, device=dev), gather=False)
+        del k1
+    if world > 1:
+        dist.barrier()
+    if rank != 0:
+        return None
+    return {"workload": f"cfg4: {desc4}", "W": W4, "H": H4, "spp": spp4, "bounces": nb4,
+            "ms_1gpu": round(t1 * 1e3, 2), "ms_n_gpus": round(tn * 1e3, 2), "n_gpus": n,
+            "msamples_per_s_n_gpus": round(W4 * H4 * spp4 / tn / 1e6, 1),
+            "efficiency": round(t1 / (n * tn), 4),
+            "measured": "one render each after a warm-up; T_N = max over ranks incl. the RCCL exchange; "
+                        "T_1 = the same frame on GPU 0 alone"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -221,14 +424,16 @@ def main():
     ap.add_argument("--scaling", default="weak", choices=("weak", "strong"),
                     help="N > 1: weak = N x the config's pixels (per-GPU work fixed), strong = the config's frame")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-strong-cfg4", action="store_true", help="N > 1: skip the strong_cfg4 object")
     ap.add_argument("--no-stats", action="store_true", help="skip the counter pass (roofline.achieved = null)")
     ap.add_argument("--no-roofline-pass", action="store_true", help="skip the 1-lane per-launch timing render")
     ap.add_argument("--roofline-only", action="store_true",
                     help="counter pass + the 1-lane timing renders only (the command profiled under profiles/)")
     ap.add_argument("--cpu-row-step", type=int, default=10)
     ap.add_argument("--sim-world", type=int, default=0,
-                    help="diagnostic: render only rank 0's rows of an N-GPU strong-scaling split of the config's "
-                         "frame, on this one GPU (not a bench line)")
+                    help="diagnostic: render only one rank's rows (cfg5sweep: variants) of an N-GPU strong-scaling "
+                         "split of the config's frame, on this one GPU (not a bench line)")
+    ap.add_argument("--sim-rank", type=int, default=0, help="--sim-world: which rank's share")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", 0))
@@ -258,6 +463,9 @@ def main():
         backend = os.environ.get("RT_BENCH_BACKEND", "nccl")
         dist.init_process_group(backend, device_id=dev if backend == "nccl" else None)
 
+    if args.config == "cfg5sweep":
+        return run_sweep(args, rank, world, dev, single_process_multi, torch, dist)
+
     import rt_amd
     from rt_amd.dist import ShardedFrame
     scene, sky_kind, cam, _, _, spp, nb, desc = CONFIGS[args.config]
@@ -277,7 +485,7 @@ def main():
     if single_process_multi:
         frame = ShardedFrame(rk, 0, 1, device=dev)  # the root's full frame; the context shards it
     else:
-        frame = ShardedFrame(rk, rank, args.sim_world or world, device=dev)
+        frame = ShardedFrame(rk, args.sim_rank if args.sim_world else rank, args.sim_world or world, device=dev)
     setup_s = time.time() - t0
     info = rk.bvh_info()
     log(f"[rank {rank}] setup {setup_s:.1f}s  devices {rk.n_devices}  frame {W}x{H}  bvh {info}")
@@ -388,6 +596,9 @@ def main():
             # verification does ~5x fewer node tests than the reference's octree walk
             roofline["ref_model_rate_GBps"] = round(ref["ref_model_bytes_per_sample"] * value * 1e6 / 1e9, 1)
 
+    strong = None
+    if n_gpus > 1 and not args.sim_world and not args.no_strong_cfg4:
+        strong = strong_cfg4(args, rk, P, sky, cam17, rank, world, dev, single_process_multi, torch, dist)
     if world > 1:
         dist.barrier()
     if rank == 0:
@@ -415,6 +626,8 @@ def main():
             "cpu_baseline": cpu,
             "parity": parity,
         }
+        if strong is not None:
+            out["strong_cfg4"] = strong
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

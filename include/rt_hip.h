@@ -107,6 +107,22 @@ int rt_render(rt_context* ctx, int width, int height, int samples, int max_bounc
 int rt_render_device(rt_context* ctx, int width, int height, int samples, int max_bounces, void* d_fb,
                      int row_offset, int row_stride, void* stream);
 
+/* The Cook-Torrance material sweep (BASELINE config 5) as replicas: n_variants
+ * material tables materials[n_variants][n_materials][10] over the bound scene
+ * (rt_set_materials semantics for each: no octree / BVH rebuild). Variant v
+ * renders rows y = row_offset + j*row_stride of its own frame on device
+ * v mod N of the context, each device walking its variants in order on its own
+ * stream; the devices run concurrently and exchange nothing. Output: either
+ * fb_rgba (host, n_variants blocks of rows_local*w*4 floats, read and overwritten
+ * like rt_render's) or d_fbs[v] (device buffers of rows_local*w*4 floats, d_fbs[v]
+ * on device v mod N). Synchronous; rt_last_kernel_ms is the slowest device's time.
+ * The context's own material table (rt_set_scene / rt_set_materials) is what the
+ * next render uses again. Replaces the caller loop of render_kernel.h:81-93
+ * (edit the bound std::vector<SimpleMaterial>, render(), repeat). */
+int rt_render_variants(rt_context* ctx, int width, int height, int samples, int max_bounces, int n_variants,
+                       const float* materials, int n_materials, int row_offset, int row_stride, float* fb_rgba,
+                       void* const* d_fbs);
+
 /* ray_trace_pixel for a list of n pixels xy[n][2]: rgba[n][4] holds each
  * pixel's framebuffer value on entry and the tone-mapped value on return. */
 int rt_render_pixels(rt_context* ctx, int width, int height, int samples, int max_bounces, const int* xy, int n,

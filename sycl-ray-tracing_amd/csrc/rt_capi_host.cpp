@@ -71,14 +71,16 @@ RtSceneView rt_host_view(const rt_context* c)
     return v;
 }
 
-bool rt_scene_has_emissive_prim(const rt_context* c)
+bool rt_table_has_emissive_prim(const rt_context* c, const RtMat* table)
 {
     for (int32_t mi : c->mat_idx) {
-        const RtMat& m = c->mats[mi];
+        const RtMat& m = table[mi];
         if (m.er > 0 || m.eg > 0 || m.eb > 0) return true;
     }
     return false;
 }
+
+bool rt_scene_has_emissive_prim(const rt_context* c) { return rt_table_has_emissive_prim(c, c->mats.data()); }
 
 extern "C" {
 
@@ -331,6 +333,29 @@ int rt_render_device(rt_context* c, int w, int h, int spp, int bounces, void* d_
     if (!d_fb || row_stride <= 0 || row_offset < 0 || row_offset >= row_stride)
         return rt_fail(c, RT_ERR_ARG, "rt_render_device: bad shard");
     return rt_backend_render(c, w, h, spp, bounces, nullptr, d_fb, row_offset, row_stride, stream);
+}
+
+int rt_render_variants(rt_context* c, int w, int h, int spp, int bounces, int n_var, const float* materials,
+                       int n_mats, int row_offset, int row_stride, float* fb, void* const* d_fbs)
+{
+    if (int r = check_ready(c, w, h, spp, bounces)) return r;
+    if (n_var <= 0 || !materials || n_mats <= 0 || (fb == nullptr) == (d_fbs == nullptr))
+        return rt_fail(c, RT_ERR_ARG, "rt_render_variants: bad buffers (exactly one of fb_rgba / d_fbs)");
+    if (row_stride <= 0 || row_offset < 0 || row_offset >= row_stride)
+        return rt_fail(c, RT_ERR_ARG, "rt_render_variants: bad row shard");
+    for (int32_t mi : c->mat_idx)
+        if (mi >= n_mats) return rt_fail(c, RT_ERR_ARG, "rt_render_variants: a material index is out of range");
+    if (d_fbs)
+        for (int v = 0; v < n_var; v++)
+            if (!d_fbs[v]) return rt_fail(c, RT_ERR_ARG, "rt_render_variants: null device buffer");
+    std::vector<RtMat> tabs((size_t)n_var * n_mats);
+    for (size_t i = 0; i < tabs.size(); i++) {
+        const float* p = materials + 10 * i;
+        tabs[i] = RtMat{p[0], p[1], p[2], p[8], p[4], p[5], p[6], p[9]};
+    }
+    const int r = rt_backend_render_variants(c, w, h, spp, bounces, n_var, tabs, n_mats, row_offset, row_stride, fb, d_fbs);
+    c->mats_dirty_only = true;  // the devices' tables hold the last variants: the next render re-sends the bound one
+    return r;
 }
 
 int rt_render_pixels(rt_context* c, int w, int h, int spp, int bounces, const int* xy, int n, float* rgba)

@@ -62,6 +62,12 @@ void rt_backend_destroy(rt_context* ctx);
 int rt_backend_upload(rt_context* ctx);
 int rt_backend_render(rt_context* ctx, int w, int h, int spp, int bounces, float* host_fb, void* dev_fb, int row_offset,
                       int row_stride, void* stream);
+// n_variants material tables (RtMat, n_mats each, back to back); variant v on device v mod N
+int rt_backend_render_variants(rt_context* ctx, int w, int h, int spp, int bounces, int n_variants,
+                               const std::vector<RtMat>& tables, int n_mats, int row_offset, int row_stride,
+                               float* host_fb, void* const* d_fbs);
+// rt_scene_has_emissive_prim for another material table over the context's material indices
+bool rt_table_has_emissive_prim(const rt_context* ctx, const RtMat* table);
 int rt_backend_render_pixels(rt_context* ctx, int w, int h, int spp, int bounces, const int* xy, int n, float* rgba);
 int rt_backend_intersect(rt_context* ctx, const float* rays, int n, void* out);
 

@@ -48,7 +48,7 @@ static void host_append(const rtk::WaveView& W, int32_t* act_count, int p, const
 }
 
 static int run_wave_host(rt_context* c, int w, int h, int spp, int bounces, const rtk::PixSrc& src, int n,
-                         float4_* fb, unsigned long long* stats_out)
+                         float4_* fb, unsigned long long* stats_out, const RtMat* mats = nullptr)
 {
     if (n <= 0) return RT_OK;
     rtk::WaveView W{};
@@ -59,6 +59,7 @@ static int run_wave_host(rt_context* c, int w, int h, int spp, int bounces, cons
     std::vector<char> arena(rtk::wave_carve(nullptr, (size_t)n, W));
     rtk::wave_carve(arena.data(), (size_t)n, W);
     W.S = rt_host_view(c);
+    if (mats) W.S.mats = mats;  // (rt_render_variants: a variant's table, same size as the bound one)
     W.cam = c->cam;
     W.src = src;
     W.W = w;
@@ -67,7 +68,7 @@ static int run_wave_host(rt_context* c, int w, int h, int spp, int bounces, cons
     W.bounces = bounces;
     rtk::set_view_consts(W);
     W.n_slots = n;
-    W.bl_rays = rt_scene_has_emissive_prim(c) ? 1 : 0;
+    W.bl_rays = rt_table_has_emissive_prim(c, W.S.mats) ? 1 : 0;
     W.any_rays = W.S.n_spheres == 0 ? 1 : 0;
     W.fb = fb;
     W.budget = RT_HOSTSIM_BUDGET;
@@ -291,6 +292,36 @@ int rt_backend_render(rt_context* c, int w, int h, int spp, int bounces, float* 
     }
     c->last_kernel_ms = (omp_get_wtime() - t0) * 1e3;
     return r;
+}
+
+// The material sweep as replicas: variant v on "device" v mod N (one host thread each,
+// rt_for_devices), every device walking its variants in order (rt_render.hip's driver).
+int rt_backend_render_variants(rt_context* c, int w, int h, int spp, int bounces, int n_var,
+                               const std::vector<RtMat>& tabs, int n_mats, int off, int stride, float* host_fb,
+                               void* const* d_fbs)
+{
+    const int N = c->devices.empty() ? 1 : (int)c->devices.size();
+    const int rows = (h - off + stride - 1) / stride;
+    const size_t npx = (size_t)rows * w;
+    const double t0 = omp_get_wtime();
+    std::vector<std::vector<unsigned long long>> dst(N, std::vector<unsigned long long>(RT_STAT_COUNT, 0));
+    const int r = rt_for_devices(c, N, [&](int d) {
+        for (int v = d; v < n_var; v += N) {
+            // (hostsim: the per-variant mats pointer must cover the context's material indices)
+            std::vector<RtMat> tab(tabs.begin() + (size_t)v * n_mats, tabs.begin() + (size_t)(v + 1) * n_mats);
+            float4_* fb = host_fb ? (float4_*)(host_fb + 4 * npx * v) : (float4_*)d_fbs[v];  // (host pointers here)
+            rtk::PixSrc src{w, off, stride, nullptr};
+            if (int e = run_wave_host(c, w, h, spp, bounces, src, (int)npx, fb, dst[d].data(), tab.data())) return e;
+        }
+        return 0;
+    });
+    c->last_kernel_ms = (omp_get_wtime() - t0) * 1e3;
+    if (r) return r;
+    for (int i = 0; i < RT_STAT_COUNT; i++) {
+        c->stats[i] = 0;
+        for (int d = 0; d < N; d++) c->stats[i] += dst[d][i];
+    }
+    return RT_OK;
 }
 
 int rt_backend_render_pixels(rt_context* c, int w, int h, int spp, int bounces, const int* xy, int n, float* rgba)

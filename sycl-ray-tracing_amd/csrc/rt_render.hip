@@ -2140,6 +2140,69 @@ int rt_backend_render(rt_context* c, int w, int h, int spp, int bounces, float* 
     return g->multi ? RT_OK : finish_stats(c, b, s);
 }
 
+// The material sweep as replicas (rt_render_variants): variant v on device v mod N, one
+// host thread per device (rt_for_devices), each device walking its variants in order on
+// its own stream: the variant's table goes into the device's material buffer with a copy
+// ordered after the previous variant's frame (same stream), then the wavefront loop.
+// No exchange between devices.
+int rt_backend_render_variants(rt_context* c, int w, int h, int spp, int bounces, int n_var,
+                               const std::vector<RtMat>& tabs, int n_mats, int off, int stride, float* host_fb,
+                               void* const* d_fbs)
+{
+    Group* g = grp(c);
+    const int N = (int)g->dev.size();
+    const int rows = (h - off + stride - 1) / stride;
+    const size_t npx = (size_t)rows * w;
+    if (npx > 0x7fffffff / 8) return rt_fail(c, RT_ERR_ARG, "render: too many pixels for one launch");
+    std::vector<float> ms(N, 0.0f);
+    const int r = rt_for_devices(c, N, [&](int d) -> int {
+        Backend* b = g->dev[d];
+        HIPCHK(c, hipSetDevice(b->device));
+        hipStream_t s = b->own;
+        if (b->done_recorded) HIPCHK(c, hipEventSynchronize(b->ev_done));  // (the table and buffers are reused)
+        if (int e = ensure(c, b->mats, (size_t)n_mats * sizeof(RtMat))) return e;
+        b->view.mats = (const RtMat*)b->mats.p;
+        b->view.n_mats = n_mats;
+        if (host_fb)
+            if (int e = ensure(c, b->fb, npx * sizeof(float4_))) return e;
+        HIPCHK(c, hipEventRecord(b->ev0, s));
+        for (int v = d; v < n_var; v += N) {
+            const RtMat* tab = tabs.data() + (size_t)v * n_mats;
+            b->bl_rays = rt_table_has_emissive_prim(c, tab) ? 1 : 0;
+            // (pageable source: the copy is staged before the call returns, and ordered on s
+            // after the previous variant's frame, whose lanes joined back into s)
+            HIPCHK(c, hipMemcpyAsync(b->mats.p, tab, (size_t)n_mats * sizeof(RtMat), hipMemcpyHostToDevice, s));
+            float4_* fb = host_fb ? (float4_*)b->fb.p : (float4_*)d_fbs[v];
+            if (host_fb)
+                HIPCHK(c, hipMemcpyAsync(fb, host_fb + 4 * npx * v, npx * sizeof(float4_), hipMemcpyHostToDevice, s));
+            const rtk::PixSrc src{w, off, stride, nullptr};
+            if (int e = run_wave(c, b, w, h, spp, bounces, src, (int)npx, fb, s)) return e;
+            if (host_fb)
+                HIPCHK(c, hipMemcpyAsync(host_fb + 4 * npx * v, fb, npx * sizeof(float4_), hipMemcpyDeviceToHost, s));
+        }
+        HIPCHK(c, hipEventRecord(b->ev1, s));
+        HIPCHK(c, hipStreamSynchronize(s));
+        HIPCHK(c, hipEventElapsedTime(&ms[d], b->ev0, b->ev1));
+        return 0;
+    });
+    // the bound table comes back with the next render's upload (rt_render_variants marks it)
+    for (Backend* b : g->dev) b->bl_rays = rt_scene_has_emissive_prim(c) ? 1 : 0;
+    HIPCHK(c, hipSetDevice(be(c)->device));
+    if (r) return r;
+    c->last_kernel_ms = *std::max_element(ms.begin(), ms.end());
+    if (c->stats_enabled) {  // (the last variant of each device, summed)
+        unsigned long long sum[2 * RT_STAT_COUNT] = {};
+        for (Backend* b : g->dev) {
+            HIPCHK(c, hipSetDevice(b->device));
+            HIPCHK(c, hipMemcpy(c->stats, b->stats.p, sizeof(c->stats), hipMemcpyDeviceToHost));
+            for (int i = 0; i < 2 * RT_STAT_COUNT; i++) sum[i] += c->stats[i];
+        }
+        std::memcpy(c->stats, sum, sizeof sum);
+        HIPCHK(c, hipSetDevice(be(c)->device));
+    }
+    return RT_OK;
+}
+
 // One device's share of a pixel list (host buffers in and out).
 static int render_pixels_one(rt_context* c, Backend* b, int w, int h, int spp, int bounces, const int* xy, int n,
                              float* rgba, float* ms_out)

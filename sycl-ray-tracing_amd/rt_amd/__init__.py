@@ -269,6 +269,35 @@ class RenderKernel:
                                               ctypes.c_void_p(stream) if stream else None), self.ctx,
               "rt_render_device")
 
+    def render_variants(self, materials, frames=None, device_ptrs=None, row_offset: int = 0, row_stride: int = 1):
+        """rt_render_variants: the material sweep as replicas. `materials` is
+        [n_variants, n_materials, 10] (or a list of [n_materials, 10] tables); variant v
+        renders rows row_offset + j*row_stride of its own frame on device v mod N of the
+        context, no exchange between devices. Output into `frames` (host float32
+        [n_variants, rows, W, 4], read-modify-written like render()), or into
+        `device_ptrs[v]` (device buffers of rows*W*4 floats, each on device v mod N).
+        Returns `frames` (host mode). The bound material table is untouched."""
+        tabs = np.ascontiguousarray(np.stack([np.asarray(m, np.float32).reshape(-1, 10) for m in materials]),
+                                    dtype=np.float32)
+        n_var, n_mats = tabs.shape[0], tabs.shape[1]
+        rows = len(range(row_offset, self.height, row_stride))
+        self._sync_materials()
+        if device_ptrs is not None:
+            assert len(device_ptrs) == n_var
+            arr = (ctypes.c_void_p * n_var)(*[ctypes.c_void_p(int(p)) for p in device_ptrs])
+            fb_p, d_p = None, ctypes.cast(arr, ctypes.c_void_p)
+        else:
+            if frames is None:
+                frames = np.zeros((n_var, rows, self.width, 4), np.float32)
+                frames[..., 3] = 1.0  # (Image's default alpha, as Image(w, h))
+            assert frames.flags.c_contiguous and frames.dtype == np.float32 and frames.shape == (n_var, rows,
+                                                                                                  self.width, 4)
+            fb_p, d_p = ptr(frames), None
+        check(self.L, self.L.rt_render_variants(self.ctx, self.width, self.height, self.render_samples,
+                                                self.max_bounces, n_var, ptr(tabs), n_mats, row_offset, row_stride,
+                                                fb_p, d_p), self.ctx, "rt_render_variants")
+        return frames
+
     def ray_trace_pixels(self, xy) -> None:
         self._sync_materials()
         xy = np.ascontiguousarray(xy, dtype=np.int32).reshape(-1, 2)

@@ -23,7 +23,7 @@ EXPORTS = [
     "rt_render_device", "rt_render_pixels", "rt_intersect", "rt_set_stats", "rt_get_stats", "rt_last_kernel_ms",
     "rt_mesh_load", "rt_mesh_counts", "rt_mesh_copy", "rt_mesh_free", "rt_camera_preset", "rt_env_luminance_cdf",
     "rt_octree_dump", "rt_read_hdr", "rt_write_png", "rt_image_to_rgba8",
-    "rt_set_intersect_mode", "rt_create_multi", "rt_device_count", "rt_set_materials",
+    "rt_set_intersect_mode", "rt_create_multi", "rt_device_count", "rt_set_materials", "rt_render_variants",
 ]
 
 # return codes (include/rt_hip.h)
@@ -52,6 +52,7 @@ _SIGS = {
     "rt_render": (I, [P, I, I, I, I, P]),
     "rt_render_device": (I, [P, I, I, I, I, P, I, I, P]),
     "rt_render_pixels": (I, [P, I, I, I, I, P, I, P]),
+    "rt_render_variants": (I, [P, I, I, I, I, I, P, I, I, I, P, P]),
     "rt_intersect": (I, [P, P, I, P]),
     "rt_set_stats": (I, [P, I]),
     "rt_set_intersect_mode": (I, [P, I]),

@@ -231,3 +231,88 @@ def test_gpu_materials_edit_between_async_renders(manifest, cameras):
         ref.render_device(b.ptr, 0, 1, None)
         np.testing.assert_array_equal(_bits(frame), _bits(b.download(init.shape, np.float32)))
     assert not np.array_equal(_bits(got[0]), _bits(got[1]))
+
+
+# ---------------------------------------------- the material sweep as replicas
+def _variant_tables(P, n=4):
+    """n Cook-Torrance variants of every material (metalness x roughness grid, cfg5-style)."""
+    out = []
+    for v in range(n):
+        m = P.materials.copy()
+        m[:, 8] = np.float32([0.0, 1.0 / 3.0, 2.0 / 3.0, 1.0][v % 4])
+        m[:, 9] = np.float32([0.05, 0.25, 0.5, 1.0][(v // 4 + v) % 4])
+        out.append(m)
+    return out
+
+
+@pytest.mark.parametrize("devices", [0, [0, 1], [0, 1, 2]])
+def test_hostsim_render_variants_match_single_renders(devices, manifest, cameras):
+    """rt_render_variants (variant v on device v mod N, no exchange): every variant's
+    frame equals a render of a fresh context built with that table; the bound table
+    is what the next plain render uses."""
+    e = rt_cases.golden_case("cornell32_128", manifest)
+    P = parsed_scene(e["scene"])
+    tabs = _variant_tables(P, 5)
+    rk, fb = rt_cases.make_kernel(e, cameras, hostsim=True, device=devices, W=48, H=40)
+    frames = rk.render_variants(tabs)
+    for v, m in enumerate(tabs):
+        ref, rfb = rt_cases.make_kernel(e, cameras, hostsim=True, W=48, H=40, materials=m.copy())
+        ref.render()
+        np.testing.assert_array_equal(_bits(frames[v]), _bits(rfb.pixels))
+    # a row shard of every variant
+    shards = rk.render_variants(tabs[:3], row_offset=1, row_stride=3)
+    np.testing.assert_array_equal(_bits(shards), _bits(frames[:3, 1::3]))
+    rk.render()  # the bound table again
+    ref, rfb = rt_cases.make_kernel(e, cameras, hostsim=True, W=48, H=40)
+    ref.render()
+    np.testing.assert_array_equal(_bits(fb.pixels), _bits(rfb.pixels))
+
+
+def test_render_variants_rejects_bad_arguments(manifest, cameras):
+    e = rt_cases.golden_case("cornell32_128", manifest)
+    P = parsed_scene(e["scene"])
+    rk, _ = rt_cases.make_kernel(e, cameras, hostsim=True, W=16, H=16)
+    with pytest.raises(rt_amd.RtError):
+        rk.render_variants([P.materials[:1]])  # a material index out of range
+    with pytest.raises(rt_amd.RtError):
+        rk.render_variants([P.materials], row_offset=2, row_stride=2)
+
+
+# golden pixels of every cfg5 variant on rows 1, 540, 1079 (sample_pixels' fixed set)
+CFG5_ROWS = (1, 539)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("devices", [0, [0, 0]])
+def test_gpu_cfg5_variants_replicas_match_goldens(devices, manifest, cameras, monkeypatch):
+    """BASELINE config 5 as replicas: the 16 material variants in one rt_render_variants
+    call (rows 1, 540, 1079 of each 1920x1080x1024spp frame), against the compiled
+    reference's goldens on every golden pixel of those rows, host and device outputs;
+    [0, 0]: two replica devices on one GPU (RT_MULTI_LOOPBACK), variants alternating."""
+    from hip_mem import DeviceBuffer
+    if isinstance(devices, list):
+        monkeypatch.setenv("RT_MULTI_LOOPBACK", "1")
+    cases = [rt_cases.golden_case(f"cfg5_sweep_m{m}_r{r}", manifest) for m in range(4) for r in range(4)]
+    P = parsed_scene(cases[0]["scene"])
+    tabs = [rt_cases.materials_for(e, P) for e in cases]
+    rk, _ = rt_cases.make_kernel(cases[0], cameras, hostsim=False, device=devices)
+    off, stride = CFG5_ROWS
+    rows = list(range(off, cases[0]["H"], stride))
+    frames = rk.render_variants(tabs, row_offset=off, row_stride=stride)
+    checked = 0
+    for v, e in enumerate(cases):
+        for (x, y), want in zip(e["px"], e["expected"]):
+            if y in rows:
+                got = frames[v, rows.index(y), x]
+                assert (got.view(np.uint32)[:3] == want.view(np.uint32)[:3]).all(), (v, x, y, got, want)
+                checked += 1
+    assert checked >= 16 * 5
+    # device outputs: the same bits
+    init = np.zeros((len(rows), cases[0]["W"], 4), np.float32)
+    init[..., 3] = 1.0
+    bufs = [DeviceBuffer(init.nbytes) for _ in tabs]
+    for b in bufs:
+        b.upload(init)
+    rk.render_variants(tabs, device_ptrs=[b.ptr for b in bufs], row_offset=off, row_stride=stride)
+    for v, b in enumerate(bufs):
+        np.testing.assert_array_equal(_bits(b.download(init.shape, np.float32)), _bits(frames[v]))
