@@ -39,15 +39,6 @@ $(LIB)/librt_hip.so: $(OBJ)/rt_render.o $(OBJ)/rt_scene.host.o $(OBJ)/rt_imageio
 	@mkdir -p $(LIB)
 	$(HIPCC) -shared --offload-arch=$(ARCH) -fPIC $^ -o $@
 
-# debug build with per-chunk timing records in k_trace (tools/chunk_trace.py); not part of `all`
-$(OBJ)/rt_render_trace.o: $(SRC)/rt_render.hip $(HDRS)
-	@mkdir -p $(OBJ)
-	$(HIPCC) $(HIPFLAGS) -DRT_CHUNK_TRACE -c $< -o $@
-
-$(LIB)/librt_hip_trace.so: $(OBJ)/rt_render_trace.o $(OBJ)/rt_scene.host.o $(OBJ)/rt_imageio.host.o $(OBJ)/rt_capi_host.host.o
-	@mkdir -p $(LIB)
-	$(HIPCC) -shared --offload-arch=$(ARCH) -fPIC $^ -o $@
-
 $(LIB)/librt_hostsim.so: $(OBJ)/rt_hostsim.o $(OBJ)/rt_scene.host.o $(OBJ)/rt_imageio.host.o $(OBJ)/rt_capi_host.host.o
 	@mkdir -p $(LIB)
 	$(CXX) -shared -fopenmp $^ -o $@

@@ -65,8 +65,6 @@ RtSceneView rt_host_view(const rt_context* c)
     v.bvh_tri4 = c->flat.bvh_tri4.data();
     v.parent = c->flat.parent.data();
     v.leaf_of = c->flat.leaf_of.data();
-    v.bvh4_ntop = c->flat.bvh4_ntop;
-    v.bvh4_top = 0;
     v.tri_mat = 0;
     return v;
 }

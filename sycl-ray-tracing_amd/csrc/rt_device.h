@@ -99,10 +99,6 @@ struct RtSceneView {
     const float4_* bvh_tri4;   // 3 records per triangle in BVH leaf order: {a.xyz, k}, {e1, leaf record}, {e2}
     const int32_t* parent;     // octree record -> parent record (-1 for the root)
     const int32_t* leaf_of;    // leaf-order triangle k -> its octree leaf record
-    // top of the search BVH: nodes [0, bvh4_ntop) are its first levels in breadth-first
-    // order (rt_scene.cpp bvh4_top_first). A kernel that stages them in LDS (rt_quad.h
-    // top_nodes_stage) sets bvh4_top in its own copy of the view; 0: read from memory.
-    int32_t bvh4_ntop, bvh4_top;
     int32_t tri_mat;  // 1: tri4[3k + 1].w holds the material index of leaf-order triangle k (device copy)
 };
 

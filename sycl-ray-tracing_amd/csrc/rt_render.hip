@@ -418,14 +418,8 @@ __global__ __launch_bounds__(256) void k_tonemap(rtk::WaveView W)
 #define RT_LDS_CAP_ANY 16
 #define RT_REFILL 16
 #define RT_QSTACK 32            // quad walks (rt_quad.h): stack entries per quad (item + key, 64 quads per block)
-#ifndef RT_COOP_LIVE
-#define RT_COOP_LIVE -1         // occlusion walks shared by idle quads once a wave's stream has run out, in the
-                                // k_trace launches of at most this many live paths (-1: never)
-#endif
-#ifndef RT_TRACE_REFILL
-#define RT_TRACE_REFILL 4       // k_trace: idle quads of a wave that trigger a refill from its query stream (0: static
-                                // 16-query chunks). r02 sweep on cfg2 (RT_VISIT_DESCEND 2): 4 / 8 -> 726 / 723 vs 678 static
-#endif
+#define RT_TRACE_REFILL 4       // k_trace: idle quads of a wave that trigger a refill from its query stream
+                                // (r02, cfg2: 4 / 8 -> 726 / 723 vs 678 Msamples/s with static 16-query chunks)
 #ifndef RT_HEAVY_CALLS
 #define RT_HEAVY_CALLS 6        // heavy class (seg_id): quad_visit calls of a walk that flag its path (0: off).
                                 // cfg2 (r02): off / 3 / 6 / 10 / 16 -> 737 / 744 / 744-748 / 740 / 735 Msamples/s;
@@ -744,152 +738,7 @@ __device__ __forceinline__ void trace_stream(const rtk::WaveView& W, const RtSce
     }
 }
 
-// k_trace's occlusion role with cooperative drains (k_trace<., true>): as trace_stream<true>,
-// and once the wave's stream has run out an idle quad takes the OLDEST stack entry of a
-// walk that still has two or more and walks that subtree for it (the occlusion answer
-// does not depend on the visit order): an occluder found by either ends both; the walk
-// is over when its own part and every helper are done. Per quad in LDS (s_coop[8 * qd]):
-// 0 bottom of its stack (entries below were taken), 1 helpers working for it, 2 found
-// (1 occluded, 2 abort: a helper's stack overflowed), 3..8 its ray.
-template <bool STATS, class QSTK>
-__device__ __forceinline__ void trace_stream_any_coop(const rtk::WaveView& W, const RtSceneView& S, QSTK& stk,
-                                                      const int* s_pre, int first, int total, int wg, int wn,
-                                                      int32_t* fbn, rtk::RayRec* fbl, int* s_coop, rtk::Stats* ps)
-{
-    const int lane = lane_id(), qd = lane >> 2, sub = lane & 3;
-    const int bq = (int)(threadIdx.x >> 2);  // block quad index: LDS stack column and s_coop record
-    const int wq0 = bq & ~15;                 // the wave's first block quad
-    int* me = s_coop + 8 * bq;
-    int cursor = 0;                     // the wave's next stream position (uniform)
-    bool exhausted = wg * 16 >= total;  // (uniform)
-    int role = 0;                       // 0 idle, 1 walking its own query, 2 helping quad `vq`
-    bool waiting = false;               // own part done, helpers still out
-    int vq = 0;
-    uint32_t target = 0;
-    rtk::QState q;
-    rtk::RayRec r;
-    for (;;) {
-        const unsigned long long bidle = __ballot(role == 0 && sub == 0);
-        if (!exhausted && (__popcll(bidle) >= RT_TRACE_REFILL || bidle == 0x1111111111111111ull)) {
-            if (role == 0) {
-                const int j = cursor + __popcll(bidle & ((1ull << (qd * 4)) - 1ull));
-                const int idx = (wg + (j >> 4) * wn) * 16 + (j & 15);
-                if (idx < total) {
-                    int kind;
-                    r = queue_item_at(W, s_pre, first + idx, kind);
-                    target = (rt_asuint(r.o.w) << 3) | (uint32_t)kind;
-                    if (forced_fallback(W, r.o, r.d)) {
-                        if (sub == 0) {
-                            r.d.w = rt_asfloat(target & 7u);
-                            fbl[atomicAdd(fbn, 1)] = r;
-                            atomicAdd(&W.r_park[target >> 3], 1);
-                        }
-                    } else if (rtk::qstate_begin<true>(q, rtk::v3of(r.o), rtk::v3of(r.d), sub, ps)) {
-                        role = 1;
-                        waiting = false;
-                        if (sub == 0) {
-                            me[0] = 0;
-                            me[1] = 0;
-                            me[2] = 0;
-                            me[3] = (int)rt_asuint(r.o.x), me[4] = (int)rt_asuint(r.o.y), me[5] = (int)rt_asuint(r.o.z);
-                            me[6] = (int)rt_asuint(r.d.x), me[7] = (int)rt_asuint(r.d.y);
-                        }
-                        if (sub == 1) s_coop[8 * 64 + bq] = (int)rt_asuint(r.d.z);
-                    } else if (sub == 0) {
-                        rtk::finish_any(W, target, false);
-                    }
-                }
-            }
-            cursor += __popcll(bidle);
-            exhausted = (wg + (cursor >> 4) * wn) * 16 >= total;
-            if (STATS && lane == 0) ps->c[RT_STAT_REFILLS]++;
-        }
-        // cooperative drain: idle quads take the oldest entry of a walk with two or more left
-        if (exhausted) {
-            const unsigned long long bfree = __ballot(role == 0 && sub == 0);
-            const bool can = role == 1 && !waiting && q.sp - me[0] >= 2;
-            const unsigned long long bvict = __ballot(can && sub == 0);
-            if (bfree && bvict) {
-                if (role == 0) {
-                    const int i = __popcll(bfree & ((1ull << (qd * 4)) - 1ull));  // this free quad's rank
-                    if (i < __popcll(bvict)) {
-                        unsigned long long v = bvict;
-                        for (int k = 0; k < i; k++) v &= v - 1;
-                        vq = wq0 + (__ffsll((long long)v) - 1) / 4;  // the i-th victim's block quad
-                        int* vr = s_coop + 8 * vq;
-                        const int bot = vr[0];
-                        const int item = (int)stk.r[bot * 64 + vq - bq];  // (QuadStack column of quad vq)
-                        q.o = rtk::v3(rt_asfloat((uint32_t)vr[3]), rt_asfloat((uint32_t)vr[4]), rt_asfloat((uint32_t)vr[5]));
-                        q.d = rtk::v3(rt_asfloat((uint32_t)vr[6]), rt_asfloat((uint32_t)vr[7]),
-                                      rt_asfloat((uint32_t)s_coop[8 * 64 + vq]));
-                        q.rb = rtk::rayb_setup(q.o, q.d);
-                        q.h.k = 0;
-                        q.sp = 0;
-                        q.bot = 0;
-                        q.cur = item;
-                        role = 2;
-                        if (sub == 0) {
-                            vr[0] = bot + 1;        // (one helper per walk and trip: no race)
-                            atomicAdd(&vr[1], 1);   // (helpers of the walk may finish in this trip)
-                        }
-                    }
-                }
-            }
-        }
-        const unsigned long long bbusy = __ballot(role != 0);
-        if (!bbusy) {
-            if (exhausted) break;
-            continue;
-        }
-        if (STATS) {
-            if (role != 0 && !waiting && sub == 0) ps->c[exhausted ? RT_STAT_DRAIN_VISITS : RT_STAT_QUAD_VISITS]++;
-            if (lane == 0) ps->c[exhausted ? RT_STAT_DRAIN_SLOTS : RT_STAT_WAVE_SLOTS] += 16;
-        }
-        const int owner = role == 2 ? vq : bq;
-        int* orec = s_coop + 8 * owner;
-        if (role != 0 && !waiting) {
-            if (orec[2] != 0) {  // the walk is decided (an occluder, or an abort) elsewhere
-                if (role == 2) {
-                    if (sub == 0) atomicSub(&orec[1], 1);
-                    role = 0;
-                } else {
-                    waiting = true;
-                }
-            } else {
-                if (role == 1) q.bot = orec[0];
-                const int res = rtk::quad_visit<true>(S, q, stk, sub, ps);
-                if (res != 0) {
-                    // bit 0: an occluder (the answer), bit 1: a stack overflowed (the exact walk decides)
-                    if (sub == 0 && (res < 0 || q.h.k == 1)) atomicOr(&orec[2], res < 0 ? 2 : 1);
-                    if (role == 2) {
-                        if (sub == 0) atomicSub(&orec[1], 1);
-                        role = 0;
-                    } else {
-                        waiting = true;
-                    }
-                }
-            }
-        }
-        if (role == 1 && waiting && orec[1] == 0) {  // own part and every helper done
-            role = 0;
-            waiting = false;
-            if (sub == 0) {
-                const int f = orec[2];
-                if (f == 2) {  // no occluder found and a part overflowed: the exact walk answers it (k_step(i))
-                    r.d.w = rt_asfloat(target & 7u);
-                    fbl[atomicAdd(fbn, 1)] = r;
-                    atomicAdd(&W.r_park[target >> 3], 1);
-                } else {
-                    rtk::finish_any(W, target, (f & 1) != 0);
-                }
-            }
-        }
-    }
-}
-
-// COOP: the occlusion role with cooperative drains (trace_stream_any_coop); the host picks
-// it for the launches of few queries, where the drain is most of the launch (RT_COOP_LIVE)
-template <bool STATS, bool COOP>
+template <bool STATS>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_OCC, 8))) void k_trace(rtk::WaveView W, int par, unsigned long long* stats)
 {
     __shared__ uint32_t s_lds[RT_LDS_WORDS * 256];
@@ -918,9 +767,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_OC
     rtk::Stats* ps = STATS ? &st : nullptr;
     const int b = (int)blockIdx.x;
 
-    // the search BVH's top levels in LDS (every walk's first trips)
-    RtSceneView S = W.S;
-    S.bvh4_top = rtk::top_nodes_stage(S);
+    const RtSceneView S = W.S;
     // fast roles: a quad of lanes per query (rt_quad.h), 16 queries per wave
     rtk::QuadStack<RT_QSTACK, 64> stk{s_lds + (threadIdx.x >> 2), (float*)s_lds + RT_QSTACK * 64 + (threadIdx.x >> 2)};
     // queue segments in stream order (seg_id: each role's heavy class first): prefix table in LDS
@@ -940,111 +787,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_OC
     const int total = closest ? nc : na;
     int32_t* fbn = cnt + (closest ? C_FBC0 : C_FBA0) + par;  // walked exactly by k_step(i)
     rtk::RayRec* fbl = closest ? W.fb_c[par] : W.fb_a[par];
-#if RT_TRACE_REFILL
     // The wave's queries are a stream (its 16-query chunks base = wg*16 + c*wn*16 in turn):
     // each quad walks one, one trip per loop (rt_quad.h quad_visit), and as soon as
     // RT_TRACE_REFILL quads are idle they all take the next queries, so a long walk holds
-    // up its own quad, not the wave's next 15 queries. Same trips and answers as the
-    // whole-walk functions.
-    if (closest) {
+    // up its own quad, not the wave's next 15 queries.
+    if (closest)
         trace_stream<false, STATS>(W, S, stk, s_pre, c0, total, wg, wn, fbn, fbl, ps);
-    } else if (COOP) {
-        __shared__ int s_coop[9 * 64];
-        trace_stream_any_coop<STATS>(W, S, stk, s_pre, a0, total, wg, wn, fbn, fbl, s_coop, ps);
-    } else {
+    else
         trace_stream<true, STATS>(W, S, stk, s_pre, a0, total, wg, wn, fbn, fbl, ps);
-    }
-#else
-    const int sub = (int)(threadIdx.x & 3);
-    for (int base = wg * 16; base < total; base += wn * 16) {
-        const int idx = base + (lane_id() >> 2);
-        bool fail = false;
-        rtk::RayRec r;
-        uint32_t target = 0;
-#ifdef RT_CHUNK_TRACE
-        // debug build: per-chunk wall time and per-lane work (tools/chunk_trace.py)
-        rtk::Stats qs;
-        for (int i = 0; i < RT_STAT_COUNT; i++) qs.c[i] = 0;
-        ps = &qs;
-        const uint64_t t_chunk = __builtin_amdgcn_s_memrealtime();
-#endif
-        const unsigned long long v0 = STATS ? st.c[RT_STAT_VOL] + st.c[RT_STAT_ANY_VOL] : 0;
-        if (idx < total) {
-            // queue item: segment (kind, shard) of global index g
-            int kind;
-            r = queue_item_at(W, s_pre, (closest ? c0 : a0) + idx, kind);
-            target = (rt_asuint(r.o.w) << 3) | (uint32_t)kind;
-            if (forced_fallback(W, r.o, r.d)) {
-                fail = sub == 0;
-            } else if (closest) {
-                float t;
-                int k;
-                if (rtk::quad_query_closest(S, rtk::v3of(r.o), rtk::v3of(r.d), stk, sub, t, k, ps)) {
-                    if (sub == 0) rtk::finish_closest(W, target, rtk::v3of(r.o), rtk::v3of(r.d), t, k);
-                } else {
-                    fail = sub == 0;
-                }
-            } else {
-                const int a = rtk::quad_query_any(S, rtk::v3of(r.o), rtk::v3of(r.d), stk, sub, ps);
-                if (a >= 0) {
-                    if (sub == 0) rtk::finish_any(W, target, a == 1);
-                } else {
-                    fail = sub == 0;
-                }
-            }
-        }
-#ifdef RT_CHUNK_TRACE
-        if (W.ctrace) {
-            const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
-            int vis = (int)((qs.c[RT_STAT_VOL] + qs.c[RT_STAT_ANY_VOL]) / 4);  // 4 box tests per node
-            int tri = (int)(qs.c[RT_STAT_TRI] + qs.c[RT_STAT_ANY_TRI]);
-            int vmax = vis, vsum = vis, tsum = tri;
-            for (int o = 32; o > 0; o >>= 1) {
-                vmax = max(vmax, __shfl_xor(vmax, o));
-                vsum += __shfl_xor(vsum, o);
-                tsum += __shfl_xor(tsum, o);
-            }
-            if (lane_id() == 0) {
-                const int rec = atomicAdd(W.ctrace_n, 1);
-                if (rec < W.ctrace_cap) {
-                    uint32_t* o = W.ctrace + 8 * (size_t)rec;
-                    unsigned xcc;
-                    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-                    o[0] = (uint32_t)(t_chunk - W.ctrace_t0);
-                    o[1] = (uint32_t)(t_end - W.ctrace_t0);
-                    o[2] = (uint32_t)vmax;
-                    o[3] = (uint32_t)vsum;
-                    o[4] = (uint32_t)tsum;
-                    o[5] = (uint32_t)(closest ? 1 : 2) | ((xcc & 15u) << 4);
-                    o[6] = (uint32_t)(blockIdx.x * 4 + (threadIdx.x >> 6));
-                    o[7] = (uint32_t)min(16, total - base);
-                }
-            }
-        }
-#endif
-        if (STATS) {  // SIMT efficiency of the chunk: its quads' visits against 16 x the longest
-            int nv = idx < total && sub == 0 ? (int)((st.c[RT_STAT_VOL] + st.c[RT_STAT_ANY_VOL] - v0) / 4) : 0;
-            int vm = nv;
-            for (int o = 32; o > 0; o >>= 1) vm = max(vm, __shfl_xor(vm, o));
-            st.c[RT_STAT_QUAD_VISITS] += nv;
-            if (lane_id() == 0) st.c[RT_STAT_WAVE_SLOTS] += 16ull * vm;
-        }
-        if (STATS && W.iterq && idx < total && sub == 0 && W.iter < RT_MAX_TIMED_ITERS) {
-            // (RT_ITER_LOG: the longest walk of the launch in node visits, per role, and
-            // how many walks took more than 24)
-            const int nv = (int)((st.c[RT_STAT_VOL] + st.c[RT_STAT_ANY_VOL] - v0) / 4);
-            int32_t* q2 = W.iterq + 2 * RT_MAX_TIMED_ITERS + 4 * W.iter;
-            atomicMax(q2 + (closest ? 0 : 1), nv);
-            if (nv > 24) atomicAdd(q2 + 2, 1);
-        }
-        const int f = wave_append(fbn, fail);
-        if (fail) {
-            r.d.w = rt_asfloat(target & 7u);
-            fbl[f] = r;
-            atomicAdd(&W.r_park[target >> 3], 1);
-        }
-    }
-#endif
     flush_stats<STATS>(st, stats);
 }
 
@@ -1081,11 +831,10 @@ __device__ __forceinline__ void tail_lists(const rtk::Emit& e, int last_kind, rt
         nl[l] += __popcll(b);
     }
 }
-#ifndef RT_TAIL_STEP_CALL
-#define RT_TAIL_STEP_CALL 1  // k_tail's path step out of line (its registers apart from the walk loop's): cfg2 811 -> 828 Msamples/s, cfg4 8-way shard 436 -> 403 ms
-#endif
-// k_tail's path step (lanes with my >= 0) and list append, out of line: bit 0 the lane's
-// path stays in flight, bits 1-10 / 11- the closest / occlusion list lengths.
+// k_tail's path step (lanes with my >= 0) and list append, out of line (its registers apart
+// from the walk loop's; inlined, the tail loop spilled across every step: cfg2 811 -> 828
+// Msamples/s, cfg4 8-way shard 436 -> 403 ms, r02): bit 0 the lane's path stays in
+// flight, bits 1-10 / 11- the closest / occlusion list lengths.
 __device__ __noinline__ int tail_step(const rtk::WaveView& W, int my, int last_kind, rtk::RayRec* l0, rtk::RayRec* l1,
                                       rtk::Stats* ps)
 {
@@ -1119,9 +868,6 @@ __device__ __noinline__ void tail_exact(const rtk::WaveView& W, int l, uint32_t 
         rtk::finish_any(W, target, T.hit);  // (begin leaves the brute-force answer in T.hit)
     }
 }
-#ifndef RT_TAIL_MIXED
-#define RT_TAIL_MIXED 1  // closest and occlusion queries of a step in one pass (quad_query_mixed)
-#endif
 #ifndef RT_TAIL_DESCEND
 #define RT_TAIL_DESCEND RT_VISIT_DESCEND  // inner-node trips per quad_visit call in k_tail
 #endif
@@ -1139,8 +885,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TAIL_OCC
     int32_t* cnt = W.counters;
     shard_prefix(cnt, RT_QSHARDS, [&](int j) { return ac_at(par, j); }, s_pre);
     const int n = s_pre[RT_QSHARDS];
-    RtSceneView S = W.S;
-    S.bvh4_top = rtk::top_nodes_stage(S);
+    const RtSceneView S = W.S;
     rtk::Stats st;
     if (STATS)
         for (int i = 0; i < RT_STAT_COUNT; i++) st.c[i] = 0;
@@ -1177,26 +922,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TAIL_OCC
         // step; the emitted rays -> the wave's LDS lists
         const long long t0 = probe ? wall_clock64() : 0;
         int nl[2];
-#if RT_TAIL_STEP_CALL
         {
             const int r = tail_step(W, my, last_kind, s_q[wv][0], s_q[wv][1], ps);
             if (!(r & 1)) my = -1;
             nl[0] = (r >> 1) & 0x3ff;
             nl[1] = r >> 11;
         }
-#else
-        {
-            rtk::Emit e;
-            e.mask = 0;
-            e.active = false;
-            e.heavy = false;
-            if (my >= 0) {
-                rtk::path_step(W, my, e, ps);
-                if (!e.active) my = -1;
-            }
-            tail_lists(e, last_kind, s_q[wv][0], s_q[wv][1], nl);
-        }
-#endif
         long long t1 = 0;
         if (probe) {
             t1 = wall_clock64();
@@ -1204,7 +935,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TAIL_OCC
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the lists are read by other lanes
         __builtin_amdgcn_wave_barrier();
-#if RT_TAIL_MIXED
         // trace: both lists in one index space, streamed over the wave's 16 quads (an idle
         // quad takes the next query at once), each quad walking its own kind a few trips
         // per call (rt_quad.h quad_visit): a step waits for its slowest query, not for
@@ -1268,47 +998,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TAIL_OCC
             const long long t2 = wall_clock64();
             tk_walk += __shfl(t2, 0) - __shfl(t1, 0);
         }
-#else
-        // trace: closest list, then occlusion list, 16 queries (quads) per pass
-        for (int l = 0; l < 2; l++) {
-            for (int base = 0; base < nl[l]; base += 16) {
-                const int qi = base + (lane >> 2);
-                if (qi < nl[l]) {
-                    const rtk::RayRec r = s_q[wv][l][qi];
-                    const uint32_t target = rt_asuint(r.d.w);
-                    const rtk::V3 o = rtk::v3of(r.o), d = rtk::v3of(r.d);
-                    bool fail;
-                    if (l == 0) {
-                        float t;
-                        int k;
-                        fail = !rtk::quad_query_closest(S, o, d, stk, sub, t, k, ps);
-                        if (!fail && sub == 0) rtk::finish_closest(W, target, o, d, t, k);
-                    } else {
-                        const int a = rtk::quad_query_any(S, o, d, stk, sub, ps);
-                        fail = a < 0;
-                        if (!fail && sub == 0) rtk::finish_any(W, target, a == 1);
-                    }
-                    if (fail && sub == 0) {  // the exact octree walk, to completion
-                        if (STATS) st.c[RT_STAT_FALLBACK]++;
-                        xs.f = stk;
-                        if (l == 0) {
-                            rtk::TravC T;
-                            if (rtk::travc_begin(W.S, T, o, d, ps))
-                                while (rtk::travc_step(W.S, T, xs, ps)) {
-                                }
-                            rtk::finish_closest(W, target, T.o, T.d, T.best_t, T.best_k);
-                        } else {
-                            rtk::TravA T;
-                            if (rtk::trava_begin(W.S, T, o, d, ps))
-                                while (rtk::trava_step(W.S, T, xs, ps)) {
-                                }
-                            rtk::finish_any(W, target, T.hit);  // (begin leaves the brute-force answer in T.hit)
-                        }
-                    }
-                }
-            }
-        }
-#endif
     }
     if (STATS && W.iterq && lane == 0 && W.iter < RT_MAX_TIMED_ITERS) atomicMax(W.iterq + 2 * W.iter + 1, rounds);
     if (probe && lane == 0) {
@@ -1376,29 +1065,31 @@ __global__ __launch_bounds__(256, 4) void k_query(RtSceneView S, const float4_* 
     }
 }
 
-// The same through the quad walks (rt_quad.h): four lanes per query.
+// The same through the product's quad walks (rt_quad.h quad_visit, k_trace's per-trip
+// code and answer): four lanes per query.
 template <bool ANY, int OCC>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, 8))) void k_query_quad(RtSceneView S, const float4_* __restrict__ rays,
                                                     float* __restrict__ out_t, int* __restrict__ out_k, int n)
 {
     __shared__ uint32_t s_lds[2 * RT_QSTACK * 64];
-    S.bvh4_top = rtk::top_nodes_stage(S);
     const int q = (int)(threadIdx.x >> 2), sub = (int)(threadIdx.x & 3);
     rtk::QuadStack<RT_QSTACK, 64> stk{s_lds + q, (float*)s_lds + RT_QSTACK * 64 + q};
     const int stride = (int)(gridDim.x * blockDim.x) >> 2;
     for (int i = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 2); i < n; i += stride) {
-        const rtk::V3 o = rtk::v3of(rays[2 * i]), d = rtk::v3of(rays[2 * i + 1]);
-        if (ANY) {
-            const int a = rtk::quad_query_any(S, o, d, stk, sub, nullptr);
-            if (sub == 0) {
-                out_t[i] = a < 0 ? -2.0f : (float)a;
+        rtk::QState qs;
+        int res = 1;
+        if (rtk::qstate_begin<ANY>(qs, rtk::v3of(rays[2 * i]), rtk::v3of(rays[2 * i + 1]), sub, nullptr))
+            do {
+                res = rtk::quad_visit<ANY>(S, qs, stk, sub, nullptr);
+            } while (res == 0);
+        float t = -1.0f;
+        int k = -1;
+        const bool ok = res > 0 && (ANY || rtk::quad_closest_answer(S, qs, sub, t, k, nullptr));
+        if (sub == 0) {
+            if (ANY) {
+                out_t[i] = ok ? (float)(qs.h.k == 1 ? 1 : 0) : -2.0f;
                 out_k[i] = 0;
-            }
-        } else {
-            float t = 0;
-            int k = 0;
-            const bool ok = rtk::quad_query_closest(S, o, d, stk, sub, t, k, nullptr);
-            if (sub == 0) {
+            } else {
                 out_t[i] = ok ? t : -2.0f;
                 out_k[i] = ok ? k : -2;
             }
@@ -1615,8 +1306,6 @@ int upload_one(rt_context* c, Backend* b, const std::vector<int32_t>& matk, bool
     v.bvh_tri4 = (const float4_*)b->bvh_tri4.p;
     v.parent = (const int32_t*)b->parent.p;
     v.leaf_of = (const int32_t*)b->leaf_of.p;
-    v.bvh4_ntop = c->flat.bvh4_ntop;
-    v.bvh4_top = 0;
     v.tri_mat = 1;
     b->view = v;
     b->bl_rays = rt_scene_has_emissive_prim(c) ? 1 : 0;
@@ -1747,8 +1436,6 @@ int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounces, cons
     if (const char* e = getenv("RT_FORCE_FALLBACK")) force_fb = std::max(0, atoi(e));
     int heavy_calls = RT_HEAVY_CALLS;
     if (const char* e = getenv("RT_HEAVY")) heavy_calls = std::max(0, atoi(e));
-    long coop_live = RT_COOP_LIVE;  // k_trace launches of at most this many live paths use the cooperative drain
-    if (const char* e = getenv("RT_COOP_LIVE")) coop_live = atol(e);
     int tail_p = 5;  // (5 paths: 15 queries, one pass of the wave's 16 quads; sweep 2-6 within 1 %)
     if (const char* e = getenv("RT_TAIL_PATHS")) tail_p = std::min(RT_TAIL_MAXP, std::max(0, atoi(e)));
     const int tail_blocks = dev_cus * RT_TAIL_OCC;  // one grid-fill of k_tail
@@ -1852,15 +1539,10 @@ int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounces, cons
             for (int k = 0; k < 3; k++)
                 if (!La.tev[k][La.it]) HIPCHK(c, hipEventCreate(&La.tev[k][La.it]));
         if (T) HIPCHK(c, hipEventRecord(La.tev[0][La.it], La.s));
-        const bool coop = La.live <= coop_live;
-        if (S && coop)
-            hipLaunchKernelGGL((k_trace<true, true>), dim3(trace_blocks_of(La)), dim3(threads), 0, La.s, W, par, stats);
-        else if (S)
-            hipLaunchKernelGGL((k_trace<true, false>), dim3(trace_blocks_of(La)), dim3(threads), 0, La.s, W, par, stats);
-        else if (coop)
-            hipLaunchKernelGGL((k_trace<false, true>), dim3(trace_blocks_of(La)), dim3(threads), 0, La.s, W, par, stats);
+        if (S)
+            hipLaunchKernelGGL(k_trace<true>, dim3(trace_blocks_of(La)), dim3(threads), 0, La.s, W, par, stats);
         else
-            hipLaunchKernelGGL((k_trace<false, false>), dim3(trace_blocks_of(La)), dim3(threads), 0, La.s, W, par, stats);
+            hipLaunchKernelGGL(k_trace<false>, dim3(trace_blocks_of(La)), dim3(threads), 0, La.s, W, par, stats);
         if (T) HIPCHK(c, hipEventRecord(La.tev[1][La.it], La.s));
         HIPCHK(c, hipGetLastError());
         return RT_OK;

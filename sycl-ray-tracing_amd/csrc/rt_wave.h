@@ -115,10 +115,6 @@ struct WaveView {
     uint32_t* fspill_r;     // per-lane spill areas of the search-BVH stacks (RT_FAST_SPILL entries)
     float* fspill_k;
     int fspill_lanes;
-    uint32_t* ctrace;       // RT_CHUNK_TRACE builds: per-chunk records of one k_trace launch (else null)
-    int32_t* ctrace_n;
-    int ctrace_cap;
-    uint64_t ctrace_t0;
     int32_t* iterq;         // stats renders: [iteration][2] = {queries, live slots} (else null)
     int iter;               // iteration of this launch
     int tail_paths;         // k_tail: paths per wave

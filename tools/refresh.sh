@@ -1,5 +1,5 @@
 #!/bin/bash
-# End-of-session measurement refresh: roofline profiles (trace, FETCH, WRITE, SQ/TCC counters),
+# Measurement refresh (GPU box): tools/refresh.sh ROOFDIR. Roofline roofline profiles (trace, FETCH, WRITE, SQ/TCC counters),
 # traffic.json, cfg2 / cfg3 bench lines, strong-scaling shard probes.
 set -o pipefail
 R=${1:-r02_roof_i}
