@@ -26,6 +26,7 @@
 
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -87,12 +88,18 @@ public:
 
     void render()  // render_kernel.cpp:189-211
     {
+        std::lock_guard<std::mutex> lk(m_mu);
         sync_materials();
         check(rt_render(m_ctx, m_width, m_height, m_render_samples, m_max_bounces, m_frame_buffer.data()));
     }
 
+    // Thread-safe like the reference's (whose render() calls it from an OpenMP parallel-for,
+    // render_kernel.cpp:189-211): calls on one kernel are serialized, since they share the
+    // context's device buffers and the material-sync state. For throughput, hand pixel
+    // batches to rt_render_pixels (or call render()) instead of one pixel per call.
     void ray_trace_pixel(int x, int y) const  // render_kernel.cpp:75-181
     {
+        std::lock_guard<std::mutex> lk(m_mu);
         const_cast<RenderKernel*>(this)->sync_materials();
         const int xy[2] = {x, y};
         Color& px = m_frame_buffer.color_data()[y * m_width + x];
@@ -145,6 +152,7 @@ private:
     Image& m_frame_buffer;
     const std::vector<SimpleMaterial>& m_materials_buffer;
     std::vector<char> m_materials_sent;
+    mutable std::mutex m_mu;  // one call on the context at a time (ray_trace_pixel is const and may be threaded)
 };
 
 #endif  // RENDER_KERNEL_HIP_H

@@ -263,32 +263,46 @@ int load_obj_serial(const std::string& path, Mesh& out, std::string& err)
 
 // Parallel form of load_obj_serial: the text is cut into chunks at line ends;
 // workers parse each chunk's vertex and face lines (faces keep their raw OBJ
-// indices and the chunk-local vertex count, for relative indices), the mtllib /
-// usemtl lines are replayed in file order on one thread (so a usemtl resolves
-// against the libraries loaded before it), and workers then emit each chunk's
-// triangles at their final offsets. The first error in file order is reported,
-// as the serial parse would stop there.
+// indices, their line offset and the chunk-local vertex count, for relative
+// indices), the mtllib / usemtl lines are replayed in file order on one thread (so
+// a usemtl resolves against the libraries loaded before it), and workers then
+// check and emit each chunk's faces at their final offsets. Every failure is
+// positioned (the byte offset of its line: a bad vertex or short face while
+// parsing, a library that does not load at its mtllib line, an out-of-range index
+// or a face of more than 4 vertices at its face line, in load_obj_serial's check
+// order), and the first in file order is reported, as the serial loader stops at
+// the first failing line.
 namespace {
+struct ObjErr {
+    size_t at = SIZE_MAX;
+    int code = 0;
+    std::string msg;
+    void set(size_t a, int c, const std::string& m)
+    {
+        if (a < at) at = a, code = c, msg = m;
+    }
+};
 struct ObjChunk {
     const char *b, *e;
     std::vector<float> verts;
-    std::vector<long> idx;         // raw OBJ indices of the chunk's faces, concatenated
-    std::vector<int> fsize, fvloc; // per face: vertex count, chunk-local vertex count before it
+    std::vector<long> idx;           // raw OBJ indices of the chunk's faces, concatenated
+    std::vector<int> fsize, fvloc;   // per face: vertex count, chunk-local vertex count before it
+    std::vector<size_t> fpos;        // per face: byte offset of its line
     struct Ev {
         int kind;  // 0 usemtl, 1 mtllib
         int face;  // chunk-local face index it precedes
+        size_t at;
         std::string name;
     };
     std::vector<Ev> ev;
-    size_t err_at = SIZE_MAX;  // byte offset of the first error
-    std::string err;
-    int err_code = 0;
+    ObjErr perr;  // the chunk's parse error (its parse stops there)
     // phase 2 results
     size_t vbase = 0, tbase = 0;
-    bool live = false;  // at or before the first chunk with a parse error
+    bool live = false;  // at or before the first chunk with a parse / library error
     std::vector<std::pair<int, int>> mat_at;  // (local face, material) transitions
     int mat0 = -1;
     std::vector<int> emissive;
+    ObjErr ferr;  // the chunk's first face error (index range, > 4 vertices)
 };
 }  // namespace
 
@@ -318,13 +332,10 @@ int load_obj(const std::string& path, Mesh& out, std::string& err)
             pos = end;
         }
     }
-    auto fail = [&](ObjChunk& C, const char* at, int code, const char* msg) {
-        if ((size_t)(at - T) < C.err_at) C.err_at = (size_t)(at - T), C.err = msg, C.err_code = code;
-    };
     parallel_for(nch, workers, [&](int c) {
         ObjChunk& C = ch[c];
         const char* p = C.b;
-        while (p < C.e && C.err_at == SIZE_MAX) {
+        while (p < C.e) {
             const char* le = (const char*)std::memchr(p, '\n', C.e - p);
             if (!le) le = C.e;
             const char* q = skip_ws(p, le);
@@ -334,7 +345,7 @@ int load_obj(const std::string& path, Mesh& out, std::string& err)
                 bool ok = true;
                 for (int i = 0; i < 3 && ok; i++) ok = read_float(q, le, v[i]);
                 if (!ok) {
-                    fail(C, p, -3, "bad vertex line");
+                    C.perr.set((size_t)(p - T), -3, "bad vertex line");
                     break;
                 }
                 C.verts.insert(C.verts.end(), v, v + 3);
@@ -353,31 +364,31 @@ int load_obj(const std::string& path, Mesh& out, std::string& err)
                     n++;
                 }
                 if (n < 3) {
-                    fail(C, p, -3, "face with fewer than 3 vertices");
+                    C.idx.resize(C.idx.size() - n);
+                    C.perr.set((size_t)(p - T), -3, "face with fewer than 3 vertices");
                     break;
                 }
-                if (n > 4) {
-                    fail(C, p, -4, "polygons with more than 4 vertices are not supported (rapidobj earcut path)");
-                    break;
-                }
-                C.fsize.push_back(n);
+                C.fsize.push_back(n);  // (> 4 vertices: an error once its indices are checked, below)
                 C.fvloc.push_back((int)(C.verts.size() / 3));
+                C.fpos.push_back((size_t)(p - T));
             } else if (q + 6 < le && (std::strncmp(q, "usemtl", 6) == 0 || std::strncmp(q, "mtllib", 6) == 0) &&
                        (q[6] == ' ' || q[6] == '\t')) {
                 const int kind = q[0] == 'u' ? 0 : 1;
                 q = skip_ws(q + 6, le);
                 std::string name(q, le);
                 while (!name.empty() && (name.back() == ' ' || name.back() == '\t' || name.back() == '\r')) name.pop_back();
-                C.ev.push_back({kind, (int)C.fsize.size(), std::move(name)});
+                C.ev.push_back({kind, (int)C.fsize.size(), (size_t)(p - T), std::move(name)});
             }
             p = le + 1;
         }
     });
-    // file order: offsets, materials (mtllib / usemtl replayed), the first parse error
+    // file order: offsets, materials (mtllib / usemtl replayed); chunks after the first
+    // parse or library error are not needed (the serial loader stops there)
     std::vector<MtlMat> mtl;
     std::unordered_map<std::string, int> names;
     int cur = -1;
     size_t vb = 0, tb = 0;
+    ObjErr first;  // the first failure in file order
     for (ObjChunk& C : ch) {
         C.vbase = vb;
         C.tbase = tb;
@@ -385,59 +396,57 @@ int load_obj(const std::string& path, Mesh& out, std::string& err)
         C.live = true;
         for (auto& ev : C.ev) {
             if (ev.kind == 1) {
-                if (int r = load_mtl(dirname_of(path) + "/" + ev.name, mtl, names, err)) return r;
+                std::string e2;
+                if (int r = load_mtl(dirname_of(path) + "/" + ev.name, mtl, names, e2)) {
+                    first.set(ev.at, r, e2);
+                    break;
+                }
             } else {
                 auto it = names.find(ev.name);
                 cur = it == names.end() ? -1 : it->second;
                 C.mat_at.push_back({ev.face, cur});
             }
         }
-        if (C.err_at != SIZE_MAX) break;  // nothing after the first error is needed
+        first.set(C.perr.at, C.perr.code, C.perr.msg);
         vb += C.verts.size() / 3;
         for (int n : C.fsize) tb += n == 3 ? 1 : 2;
+        if (first.at != SIZE_MAX) break;
     }
-    // (a parse error stops the serial loader there; faces before it may still fail the
-    // index check first, which the emit pass below reports by position)
-    size_t first_err = SIZE_MAX;
-    std::string first_msg;
-    int first_code = 0;
-    for (ObjChunk& C : ch)
-        if (C.err_at != SIZE_MAX) {
-            first_err = C.err_at, first_msg = C.err, first_code = C.err_code;
-            break;
-        }
     std::vector<float> pos(3 * vb);
     out.tris.resize(9 * tb);
     out.mat_idx.resize(tb);
     parallel_for(nch, workers, [&](int c) {
         const ObjChunk& C = ch[c];
-        if (C.live && C.vbase * 3 + C.verts.size() <= pos.size())
-            std::memcpy(pos.data() + 3 * C.vbase, C.verts.data(), C.verts.size() * 4);
+        if (C.live) std::memcpy(pos.data() + 3 * C.vbase, C.verts.data(), C.verts.size() * 4);
     });
-    std::vector<size_t> idx_err(nch, SIZE_MAX);
+    const size_t stop_at = first.at;  // faces at or after it are never reached by the serial loader
     parallel_for(nch, workers, [&](int c) {
         ObjChunk& C = ch[c];
-        if (!C.live) return;  // (past the first parse error)
+        if (!C.live) return;
         size_t t = C.tbase, o = 0;
         size_t m = 0;
         int mat = C.mat0;
-        for (size_t f = 0; f < C.fsize.size(); f++) {
+        for (size_t f = 0; f < C.fsize.size() && C.fpos[f] < stop_at; f++) {
             while (m < C.mat_at.size() && C.mat_at[m].first <= (int)f) mat = C.mat_at[m++].second;
             const int n = C.fsize[f];
             const long nv = (long)(C.vbase + C.fvloc[f]);
             int face[4];
             bool bad = false;
-            for (int k = 0; k < n; k++) {
+            for (int k = 0; k < n; k++) {  // (load_obj_serial: the index range first, then the vertex count)
                 const long v = C.idx[o + k];
-                face[k] = v > 0 ? (int)(v - 1) : (int)(nv + v);
-                if (face[k] < 0 || face[k] >= nv) bad = true;
+                const int i = v > 0 ? (int)(v - 1) : (int)(nv + v);
+                if (i < 0 || i >= nv) bad = true;
+                if (k < 4) face[k] = i;
             }
             o += n;
             if (bad) {
-                idx_err[c] = f;
+                C.ferr.set(C.fpos[f], -3, "face index out of range");
                 return;
             }
-            if (t + (n == 3 ? 1 : 2) > tb) return;  // (the chunk holding the parse error: faces past tb)
+            if (n > 4) {
+                C.ferr.set(C.fpos[f], -4, "polygons with more than 4 vertices are not supported (rapidobj earcut path)");
+                return;
+            }
             auto emit = [&](int i0, int i1, int i2) {
                 const int id[3] = {i0, i1, i2};
                 for (int k = 0; k < 3; k++) std::memcpy(&out.tris[9 * t + 3 * k], &pos[3 * (size_t)id[k]], 12);
@@ -465,18 +474,10 @@ int load_obj(const std::string& path, Mesh& out, std::string& err)
             }
         }
     });
-    for (int c = 0; c < nch; c++) {
-        // an out-of-range index in chunk c comes before any parse error in a later chunk
-        if (ch[c].err_at != SIZE_MAX && idx_err[c] == SIZE_MAX) break;
-        if (idx_err[c] != SIZE_MAX) {
-            err = "face index out of range";
-            return -3;
-        }
-        if (ch[c].err_at != SIZE_MAX) break;
-    }
-    if (first_err != SIZE_MAX) {
-        err = first_msg;
-        return first_code;
+    for (const ObjChunk& C : ch) first.set(C.ferr.at, C.ferr.code, C.ferr.msg);
+    if (first.at != SIZE_MAX) {
+        err = first.msg;
+        return first.code;
     }
     for (const ObjChunk& C : ch) out.emissive.insert(out.emissive.end(), C.emissive.begin(), C.emissive.end());
     // SimpleMaterial list (utils.cpp:73-95)

@@ -5,7 +5,8 @@
 // render(). Container test (tests/test_shim.py): linked against librt_hostsim.so (the
 // same C ABI; the GPU box has no /root/reference). Writes the frame, then checks the
 // by-reference material semantics: an in-place edit of the material vector between
-// renders gives the frame a fresh kernel over the edited vector gives.
+// renders gives the frame a fresh kernel over the edited vector gives, and ray_trace_pixel
+// called from an OpenMP parallel-for (the reference's render() loop) gives render()'s frame.
 //   shim_test <obj> <sky.raw> <camera> W H spp bounces <out.f32>
 #include <cstdio>
 #include <cstdlib>
@@ -77,7 +78,18 @@ int main(int argc, char** argv)
     fb[py * W + px] = Color();
     rk.ray_trace_pixel(px, py);
     const bool pixel_ok = std::memcmp(&fb[py * W + px], &want, 16) == 0 || (want.r != want.r);
-    std::printf("SHIM devices %d materials_by_reference %d changed %d pixel %d\n", rk.device_count(), same ? 1 : 0,
-                edited ? 1 : 0, pixel_ok ? 1 : 0);
-    return same && edited && pixel_ok ? 0 : 1;
+    // the reference's own render() pattern (render_kernel.cpp:189-211): ray_trace_pixel from an
+    // OpenMP parallel-for over rows, on one kernel (its calls serialize on the context)
+    // (every 8th row: one pixel per call is the slow way to drive a context)
+    const std::vector<float> after(fb.data(), fb.data() + (size_t)W * H * 4);
+    fb = Image(W, H);
+#pragma omp parallel for schedule(dynamic)
+    for (int y = 0; y < H; y += 8)
+        for (int x = 0; x < W; x++) rk.ray_trace_pixel(x, y);
+    bool threaded_ok = true;
+    for (int y = 0; y < H; y += 8)
+        threaded_ok = threaded_ok && std::memcmp(fb.data() + (size_t)y * W * 4, after.data() + (size_t)y * W * 4, (size_t)W * 16) == 0;
+    std::printf("SHIM devices %d materials_by_reference %d changed %d pixel %d threaded %d\n", rk.device_count(),
+                same ? 1 : 0, edited ? 1 : 0, pixel_ok ? 1 : 0, threaded_ok ? 1 : 0);
+    return same && edited && pixel_ok && threaded_ok ? 0 : 1;
 }

@@ -39,7 +39,7 @@ def _err(path):
         rt_amd.parse_obj(path)
         return None
     except rt_amd.RtError as e:
-        return str(e).split(":", 1)[1].strip()
+        return str(e)  # (the return code and the message)
 
 
 def _grid(n):
@@ -49,7 +49,8 @@ def _grid(n):
     return out
 
 
-@pytest.mark.parametrize("case", ["index_then_vertex", "vertex_then_index", "polygon", "ok"])
+@pytest.mark.parametrize("case", ["index_then_vertex", "vertex_then_index", "polygon", "ok", "index_then_parse_same_chunk",
+                                  "polygon_with_bad_index", "index_then_mtllib", "mtllib_then_index", "short_face"])
 def test_chunked_parse_first_error_in_file_order(case, tmp_path, monkeypatch):
     lines = _grid(400)
     if case == "index_then_vertex":
@@ -60,6 +61,19 @@ def test_chunked_parse_first_error_in_file_order(case, tmp_path, monkeypatch):
         lines[1500] = "f 1 2 99999"
     elif case == "polygon":
         lines[700] = "f 1 2 3 4 5"
+    elif case == "index_then_parse_same_chunk":  # (the parse error's chunk skipped its index checks)
+        lines[100] = "f 1 2 99999"
+        lines[104] = "v 1 2"
+    elif case == "polygon_with_bad_index":  # load_obj_serial checks the index range before the vertex count
+        lines[700] = "f 1 2 3 99999 5"
+    elif case == "index_then_mtllib":
+        lines[100] = "f 1 2 99999"
+        lines[1500] = "mtllib no_such_library.mtl"
+    elif case == "mtllib_then_index":
+        lines[100] = "mtllib no_such_library.mtl"
+        lines[1500] = "f 1 2 99999"
+    elif case == "short_face":
+        lines[900] = "f 1 2"
     path = _obj(tmp_path, lines)
     serial = _err(path)
     monkeypatch.setenv("RT_OBJ_PARALLEL_MIN", "0")

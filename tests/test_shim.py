@@ -32,6 +32,6 @@ def test_cpp_shim_renders_cfg1_bit_exact(manifest, tmp_path):
                        capture_output=True, text=True)
     print(r.stdout, r.stderr)
     assert r.returncode == 0, r.stdout + r.stderr
-    assert "materials_by_reference 1 changed 1 pixel 1" in r.stdout
+    assert "materials_by_reference 1 changed 1 pixel 1 threaded 1" in r.stdout
     fb = np.fromfile(out, dtype="<f4").reshape(e["H"], e["W"], 4)
     np.testing.assert_array_equal(fb.view(np.uint32), e["expected"].view(np.uint32))
