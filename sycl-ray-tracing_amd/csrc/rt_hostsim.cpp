@@ -8,6 +8,7 @@
 // librt_hip.so has no CPU path and fails loudly without a device.
 #include <omp.h>
 
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -53,6 +54,8 @@ static int run_wave_host(rt_context* c, int w, int h, int spp, int bounces, cons
     if (n <= 0) return RT_OK;
     rtk::WaveView W{};
     W.park_cap = 1 << 14;
+    W.spec_cam = 1;
+    if (const char* e = getenv("RT_SPEC_CAM")) W.spec_cam = atoi(e) != 0;
     W.spill_lanes = 0;  // the host threads keep their own spill areas
     W.shards = 1;       // one segment per queue (plain atomics on the host)
     W.seg_cap = n;
@@ -89,7 +92,7 @@ static int run_wave_host(rt_context* c, int w, int h, int spp, int bounces, cons
         host_append(W, &act[0], p, e);
     }
     using FAST = rtk::ArrayStack<RT_HOSTSIM_SHORT_CAP>;
-    const int last_kind = W.any_rays ? rtk::RK_BL : rtk::RK_BENV;
+    const int last_kind = W.any_rays ? rtk::RK_CAM : rtk::RK_BENV;
     int32_t fbc[2] = {0, 0}, fba[2] = {0, 0};
     for (long it = 0;; it++) {
         const int par = (int)(it & 1);

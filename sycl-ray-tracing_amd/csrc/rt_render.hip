@@ -114,7 +114,7 @@ __host__ __device__ __forceinline__ int hc_at(int par, int kind, int shard)
 // trips) start at the head of every wave's stream instead of setting its drain:
 //   [closest kinds' heavy shards][closest kinds' shards][occlusion kinds' heavy][occlusion kinds']
 // then zero-count padding to a multiple of 64 (shard_prefix).
-#define RT_NCK 3  // closest kinds: CONT, LSH, BL
+#define RT_NCK 4  // closest kinds: CONT, LSH, BL, CAM
 #define RT_SEG_CH (RT_NCK * RT_HSHARDS)
 #define RT_SEG_AH (RT_SEG_CH + RT_NCK * RT_QSHARDS)
 #define RT_SEG_A (RT_SEG_AH + (rtk::RK_COUNT - RT_NCK) * RT_HSHARDS)
@@ -895,7 +895,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TAIL_OCC
     const size_t gl = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     rtk::SpillStack<rtk::QuadStack<RT_QSTACK, 64>> xs{stk, W.spill_r + gl * RT_STACK_CAP, W.spill_k + gl * RT_STACK_CAP};
     const int P = W.tail_paths;
-    const int last_kind = W.any_rays ? rtk::RK_BL : rtk::RK_BENV;
+    const int last_kind = W.any_rays ? rtk::RK_CAM : rtk::RK_BENV;
     int my = -1;
     bool drained = false;
     int rounds = 0;  // (RT_ITER_LOG: the longest pool loop of the launch)
@@ -1436,6 +1436,8 @@ int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounces, cons
     if (const char* e = getenv("RT_FORCE_FALLBACK")) force_fb = std::max(0, atoi(e));
     int heavy_calls = RT_HEAVY_CALLS;
     if (const char* e = getenv("RT_HEAVY")) heavy_calls = std::max(0, atoi(e));
+    int spec_cam = 1;  // the next sample's camera ray traced ahead (rt_wave.h next_camera); RT_SPEC_CAM=0: off
+    if (const char* e = getenv("RT_SPEC_CAM")) spec_cam = atoi(e) != 0;
     int tail_p = 5;  // (5 paths: 15 queries, one pass of the wave's 16 quads; sweep 2-6 within 1 %)
     if (const char* e = getenv("RT_TAIL_PATHS")) tail_p = std::min(RT_TAIL_MAXP, std::max(0, atoi(e)));
     const int tail_blocks = dev_cus * RT_TAIL_OCC;  // one grid-fill of k_tail
@@ -1473,6 +1475,7 @@ int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounces, cons
         rtk::WaveView& W = La.W;
         W.park_cap = 1 << 16;
         W.heavy_calls = heavy_calls;
+        W.spec_cam = spec_cam;
         W.shards = RT_QSHARDS;
         W.seg_cap = 64 * (((La.n + 63) / 64 + RT_QSHARDS - 1) / RT_QSHARDS);  // (append_emit: chunks per shard)
         W.spill_lanes = dev_cus * 4 * threads;  // exact walks: up to dev_cus * 2 blocks per role

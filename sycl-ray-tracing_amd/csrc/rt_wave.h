@@ -24,7 +24,9 @@
 
 namespace rtk {
 
-enum RayKind { RK_CONT = 0, RK_LSH = 1, RK_BL = 2, RK_ESH = 3, RK_BENV = 4, RK_COUNT = 5 };
+// Closest-hit kinds first (CONT .. CAM), then the occlusion kinds (ESH, BENV): the trace
+// kernels split the queues there. CAM is the next sample's camera ray, traced ahead (below).
+enum RayKind { RK_CONT = 0, RK_LSH = 1, RK_BL = 2, RK_CAM = 3, RK_ESH = 4, RK_BENV = 5, RK_COUNT = 6 };
 
 enum PathFlag : uint32_t {
     PF_CONT = 1u,        // a continuation / camera ray is in flight
@@ -35,7 +37,9 @@ enum PathFlag : uint32_t {
     PF_ESH = 32u,        // env shadow ray emitted
     PF_BENV = 64u,       // BRDF->env ray emitted
     PF_EMIT0 = 128u,     // bounce 0: add the material emission at resolve
+    PF_CAM = 256u,       // the next sample's camera ray is in flight (next_camera)
 };
+#define RT_FLAG_BITS 12  // p_rd.w = flags | bounce << RT_FLAG_BITS
 
 struct RayRec {  // 32 B queue entry
     float4_ o;  // xyz origin, w = target (slot) bits
@@ -75,7 +79,7 @@ struct WaveView {
     int fb_rs;              // row sources: framebuffer rows from one slot row to the next (lanes alternate rows)
     // path state
     float4_* p_ro;          // ro.xyz, rng bits
-    float4_* p_rd;          // rd.xyz, flags | bounce << 8
+    float4_* p_rd;          // rd.xyz, flags | bounce << RT_FLAG_BITS
     float4_* p_thr;         // thr.rgb, sample
     float4_* p_sc;          // sc.rgb
     float4_* p_fin;         // fin.rgb
@@ -91,6 +95,8 @@ struct WaveView {
     // query results
     float* r_cont_t;
     int32_t* r_cont_k;
+    float* r_cam_t;         // the next sample's camera ray (RK_CAM), traced ahead
+    int32_t* r_cam_k;
     float* r_lsh_t;
     float* r_bl_t;
     int32_t* r_bl_k;
@@ -100,9 +106,10 @@ struct WaveView {
     RayRec* q[RK_COUNT];    // [shards * seg_cap] each, then (heavy class on) as many of its heavy class
     uint8_t* r_heavy;       // [n_slots] (heavy class on) a query of the slot took >= heavy_calls quad trips
     int heavy_calls;        // k_trace's heavy threshold (0: heavy class off; set before wave_carve)
+    int spec_cam;           // 1: trace the next sample's camera ray ahead (next_camera); 0: at the sample's start
     int32_t* counters;      // queue sizes, tickets, live counts (rt_render.hip C_*)
     int32_t* r_park;        // [n_slots] queries of the slot parked (the step skips the slot while > 0)
-    RayRec* fb_c[2];        // [5 n_slots] closest-hit queries left to the exact walk (d.w = kind), by parity
+    RayRec* fb_c[2];        // [RK_COUNT n_slots] closest-hit queries left to the exact walk (d.w = kind), by parity
     RayRec* fb_a[2];        // [2 n_slots] occlusion queries left to the exact walk, by parity
     ParkC* park_c[2];       // parked closest-hit queries, double-buffered by iteration parity
     int32_t* done[2];       // slots whose exact walks finished, by parity (released by the next k_trace)
@@ -153,6 +160,8 @@ inline size_t wave_carve(char* base, size_t n, WaveView& W)  // uses W.park_cap,
     W.q_thr = (float4_*)take(n * 16);
     W.r_cont_t = (float*)take(n * 4);
     W.r_cont_k = (int32_t*)take(n * 4);
+    W.r_cam_t = (float*)take(n * 4);
+    W.r_cam_k = (int32_t*)take(n * 4);
     W.r_lsh_t = (float*)take(n * 4);
     W.r_bl_t = (float*)take(n * 4);
     W.r_bl_k = (int32_t*)take(n * 4);
@@ -165,7 +174,7 @@ inline size_t wave_carve(char* base, size_t n, WaveView& W)  // uses W.park_cap,
     W.act_out = (int32_t*)take(qn * 4);
     W.r_park = (int32_t*)take(n * 4);
     for (int k = 0; k < 2; k++) {
-        W.fb_c[k] = (RayRec*)take(5 * n * sizeof(RayRec));
+        W.fb_c[k] = (RayRec*)take((size_t)RK_COUNT * n * sizeof(RayRec));
         W.fb_a[k] = (RayRec*)take(2 * n * sizeof(RayRec));
         W.park_c[k] = (ParkC*)take((size_t)W.park_cap * sizeof(ParkC));
         W.park_a[k] = (ParkA*)take((size_t)W.park_cap * sizeof(ParkA));
@@ -243,8 +252,8 @@ RT_HD void load_path(const WaveView& W, int p, PathReg& P)
     P.rng.a = rt_asuint(a.w);
     P.rd = v3of(b);
     const uint32_t fb = rt_asuint(b.w);
-    P.flags = fb & 0xffu;
-    P.bounce = (int)(fb >> 8);
+    P.flags = fb & ((1u << RT_FLAG_BITS) - 1u);
+    P.bounce = (int)(fb >> RT_FLAG_BITS);
     P.thr = colof(c);
     P.sample = (int)rt_asuint(c.w);
     P.sc = colof(d);
@@ -255,10 +264,46 @@ RT_HD void load_path(const WaveView& W, int p, PathReg& P)
 RT_HD void store_path(const WaveView& W, int p, const PathReg& P, bool fin_changed)
 {
     W.p_ro[p] = f4(P.ro, rt_asfloat(P.rng.a));
-    W.p_rd[p] = f4(P.rd, rt_asfloat(P.flags | ((uint32_t)P.bounce << 8)));
+    W.p_rd[p] = f4(P.rd, rt_asfloat(P.flags | ((uint32_t)P.bounce << RT_FLAG_BITS)));
     W.p_thr[p] = f4(P.thr, rt_asfloat((uint32_t)P.sample));
     W.p_sc[p] = f4(P.sc, 0.0f);
     if (fin_changed) W.p_fin[p] = f4(P.fin, 0.0f);
+}
+
+// Camera ray of a sample (render_kernel.cpp:88-92, get_camera_ray :56-73): the two
+// jitter draws from rng, then the ray.
+RT_HD void camera_ray(const WaveView& W, int x, int y, Rng& rng, V3& o, V3& d)
+{
+    float xj = ((float)x + 0.5f) + rng.next() - 1.0f;
+    float yj = ((float)y + 0.5f) + rng.next() - 1.0f;
+    float xn = xj / (float)W.W * 2.0f - 1.0f;
+    xn *= W.aspect;
+    float yn = yj / (float)W.H * 2.0f - 1.0f;
+    o = v3(W.cam_o[0], W.cam_o[1], W.cam_o[2]);
+    const V3 pd = xform_point(W.cam, v3(xn, yn, W.cam.fov_dist));
+    d = normalize(sub(pd, o));
+}
+
+// The next sample's camera ray, traced ahead. A sample's draws all happen at its
+// shaded bounces, so once a bounce is shaded the RNG state the next sample starts
+// from is known if the sample ends there: when the bounce loop ends at this bounce
+// (terminated, or the last bounce) it is certain, and when the continuation ray is
+// cast it is right exactly when that ray misses (a miss draws nothing), which is how
+// most samples end. Casting the next camera ray from a copy of the state beside the
+// bounce's own rays lets the step that sees the sample end shade the next sample's
+// first hit at once: one step per sample fewer on the path's dependent chain. When
+// the continuation hits instead, the camera answer is dropped. The ray is computed
+// again, bit for bit the same, when its sample starts (begin_sample_ahead).
+RT_HD void next_camera(const WaveView& W, int p, const PathReg& P, Emit& e, uint32_t& fl)
+{
+    if (!W.spec_cam || P.sample + 1 >= W.spp) return;
+    int x, y;
+    pix_xy(W.src, p, x, y);
+    Rng r = P.rng;
+    V3 o, d;
+    camera_ray(W, x, y, r, o, d);
+    emit(e, RK_CAM, p, o, d);
+    fl |= PF_CAM;
 }
 
 // Camera ray of the next sample (render_kernel.cpp:88-92, get_camera_ray
@@ -270,15 +315,7 @@ RT_HD bool start_sample(const WaveView& W, int p, PathReg& P, Emit& e)
     int x, y;
     pix_xy(W.src, p, x, y);
     for (;;) {
-        float xj = ((float)x + 0.5f) + P.rng.next() - 1.0f;
-        float yj = ((float)y + 0.5f) + P.rng.next() - 1.0f;
-        float xn = xj / (float)W.W * 2.0f - 1.0f;
-        xn *= W.aspect;
-        float yn = yj / (float)W.H * 2.0f - 1.0f;
-        const V3 o = v3(W.cam_o[0], W.cam_o[1], W.cam_o[2]);
-        const V3 pd = xform_point(W.cam, v3(xn, yn, W.cam.fov_dist));
-        P.ro = o;
-        P.rd = normalize(sub(pd, o));
+        camera_ray(W, x, y, P.rng, P.ro, P.rd);
         P.thr = col(1.0f);
         P.sc = col(0.0f);
         P.bounce = 0;
@@ -286,11 +323,26 @@ RT_HD bool start_sample(const WaveView& W, int p, PathReg& P, Emit& e)
         if (W.bounces > 0) {
             P.flags = PF_CONT;
             emit(e, RK_CONT, p, P.ro, P.rd);
+            // (and the one after it, should this camera ray miss: no draws, so it starts here)
+            next_camera(W, p, P, e, P.flags);
             return true;
         }
         P.fin = cadd(P.fin, P.sc);
         if (++P.sample == W.spp) return false;
     }
+}
+
+// A sample whose camera ray was traced ahead (next_camera): its draws and ray, as
+// start_sample computes them, and its camera answer is the continuation to consume.
+RT_HD void begin_sample_ahead(const WaveView& W, int p, PathReg& P)
+{
+    int x, y;
+    pix_xy(W.src, p, x, y);
+    camera_ray(W, x, y, P.rng, P.ro, P.rd);
+    P.thr = col(1.0f);
+    P.sc = col(0.0f);
+    P.bounce = 0;
+    P.flags = PF_CONT;
 }
 
 // The per-render constants of start_sample, evaluated once (same operations, so the
@@ -555,6 +607,7 @@ RT_HD void shade(const WaveView& W, int p, PathReg& P, const Hit& h, Emit& e, St
             fl |= PF_END;  // the bounce loop is over
         }
     }
+    next_camera(W, p, P, e, fl);  // (the next sample starts from this state if the sample ends here)
     P.flags = fl;
 }
 
@@ -632,8 +685,10 @@ RT_HD void resolve(const WaveView& W, int p, PathReg& P, const ResolveRec& R, St
 }
 
 // One iteration of path slot p: resolve the bounce shaded last iteration,
-// consume the continuation query, shade the new hit or end the sample,
-// start the next sample. Fills `e` with the rays for the next trace.
+// consume the continuation query, shade the new hit or end the sample; a sample
+// that ends goes on with the next one: its camera answer, when it was traced ahead
+// (next_camera), is consumed in the same step (shaded, or that sample ends too), else
+// its camera ray is cast. Fills `e` with the rays for the next trace.
 RT_HD void path_step(const WaveView& W, int p, Emit& e, Stats* st)
 {
     e.mask = 0;
@@ -646,6 +701,8 @@ RT_HD void path_step(const WaveView& W, int p, Emit& e, Stats* st)
     load_path(W, p, P);
     const float cont_t = W.r_cont_t[p];
     const int cont_k = W.r_cont_k[p];
+    const float cam_t = W.r_cam_t[p];  // (read only with PF_CAM)
+    const int cam_k = W.r_cam_k[p];
     if (park != 0) return;  // a query of this path is parked: wait
     if (heavy) {  // its last walk was long: this step's rays head the next streams
         e.heavy = true;
@@ -655,11 +712,14 @@ RT_HD void path_step(const WaveView& W, int p, Emit& e, Stats* st)
     const uint32_t fl0 = P.flags;
     ResolveRec R;
     if (fl0 & PF_AUX) resolve_load(W, p, fl0, R);
+    // (the triangle the step shades: the continuation's hit, else the next sample's camera hit)
     float4_ tr0 = float4_{0.0f, 0.0f, 0.0f, 0.0f}, tr1 = tr0, tr2 = tr0;
-    if ((fl0 & PF_CONT) && cont_t > 0.0f && cont_k >= 0) {
-        tr0 = W.S.tri4[3 * cont_k];
-        tr1 = W.S.tri4[3 * cont_k + 1];
-        tr2 = W.S.tri4[3 * cont_k + 2];
+    const bool cont_hit = (fl0 & PF_CONT) && cont_t > 0.0f && cont_k >= 0;
+    const int tk = cont_hit ? cont_k : ((fl0 & PF_CAM) && cam_t > 0.0f && cam_k >= 0) ? cam_k : -1;
+    if (tk >= 0) {
+        tr0 = W.S.tri4[3 * tk];
+        tr1 = W.S.tri4[3 * tk + 1];
+        tr2 = W.S.tri4[3 * tk + 2];
     }
     if (fl0 & PF_AUX) resolve(W, p, P, R, st);
     bool end = (P.flags & PF_END) != 0;
@@ -676,15 +736,29 @@ RT_HD void path_step(const WaveView& W, int p, Emit& e, Stats* st)
         if (P.bounce == 0 && W.bounces >= 2) P.sc = cadd(P.sc, cmul(env_from_dir(W.S, P.rd, st), P.thr));
         end = true;
     }
-    if (end) {
+    bool ahead = (fl0 & PF_CAM) != 0;  // the next sample's camera answer is here
+    while (end) {
         P.fin = cadd(P.fin, P.sc);
         if (++P.sample == W.spp) {
             e.active = false;
-        } else {
-            e.active = start_sample(W, p, P, e);
+            break;
         }
-        if (!e.active) finish_pixel(W, p, P);
+        if (!ahead) {
+            e.active = start_sample(W, p, P, e);
+            break;
+        }
+        // the next sample, its camera ray traced ahead: consume its answer now
+        ahead = false;
+        begin_sample_ahead(W, p, P);
+        Hit h;
+        if (hit_from_rec(W.S, P.ro, P.rd, cam_t, cam_k, tr0, tr1, tr2, h)) {
+            shade(W, p, P, h, e, st);
+            store_path(W, p, P, true);
+            return;
+        }
+        if (W.bounces >= 2) P.sc = cadd(P.sc, cmul(env_from_dir(W.S, P.rd, st), P.thr));  // (bounce 0 missed)
     }
+    if (!e.active) finish_pixel(W, p, P);
     store_path(W, p, P, end);
 }
 
@@ -723,6 +797,9 @@ RT_HD void finish_closest(const WaveView& W, uint32_t target, V3 o, V3 d, float 
     if (kind == RK_CONT) {
         W.r_cont_t[slot] = t;
         W.r_cont_k[slot] = k;
+    } else if (kind == RK_CAM) {
+        W.r_cam_t[slot] = t;
+        W.r_cam_k[slot] = k;
     } else if (kind == RK_LSH) {
         W.r_lsh_t[slot] = t;
     } else if (kind == RK_BL) {
