@@ -44,7 +44,7 @@ static void merge_stats(unsigned long long* out, const std::vector<rtk::Stats>& 
 static void host_append(const rtk::WaveView& W, int32_t* act_count, int p, const rtk::Emit& e)
 {
     for (int k = 0; k < rtk::RK_COUNT; k++)
-        if ((e.mask >> k) & 1u) W.q[k][__atomic_fetch_add(&W.counters[k], 1, __ATOMIC_RELAXED)] = e.r[k];
+        if ((e.mask >> k) & 1u) W.q[k][__atomic_fetch_add(&W.counters[k], 1, __ATOMIC_RELAXED)] = e.rec(k, p);
     if (e.active) W.act_out[__atomic_fetch_add(act_count, 1, __ATOMIC_RELAXED)] = p;
 }
 

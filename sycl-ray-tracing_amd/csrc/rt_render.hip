@@ -285,7 +285,7 @@ __device__ __forceinline__ void append_emit(const rtk::WaveView& W, int pout, in
             const int i = __shfl(r[k], 0) + __popcll(b[k] & lt);
             const int ih = __shfl(r[rtk::RK_COUNT + k], 0) + __popcll(b[rtk::RK_COUNT + k] & lt);
             if ((e.mask >> k) & 1u) {
-                W.q[k][kk == k ? seg + i : hseg + ih] = e.r[k];
+                W.q[k][kk == k ? seg + i : hseg + ih] = e.rec(k, p);
             }
         }
         const int a = __shfl(r[2 * rtk::RK_COUNT], 0) + __popcll(b[2 * rtk::RK_COUNT] & lt);
@@ -309,7 +309,7 @@ __device__ __forceinline__ void append_emit(const rtk::WaveView& W, int pout, in
 #pragma unroll
     for (int k = 0; k < rtk::RK_COUNT; k++) {
         const int i = __shfl(r[k], 0) + __popcll(b[k] & lt);
-        if ((e.mask >> k) & 1u) W.q[k][seg + i] = e.r[k];
+        if ((e.mask >> k) & 1u) W.q[k][seg + i] = e.rec(k, p);
     }
     const int a = __shfl(r[rtk::RK_COUNT], 0) + __popcll(b[rtk::RK_COUNT] & lt);
     if (e.active) W.act_out[seg + a] = p;
@@ -811,9 +811,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_OC
 // Entry condition (run_wave): no query is parked or waiting for the exact
 // walk, so every path is ready to step; a query the quad walk cannot answer
 // is answered here by the exact walk, inline, by lane 0 of its quad.
-#define RT_TAIL_MAXP 16  // paths per wave at most (5 rays each: 80 per list)
+#define RT_TAIL_MAXP 16  // paths per wave at most (RK_COUNT rays each per list)
 // k_tail: a path's emitted rays -> the wave's LDS lists (l0: closest-hit kinds, l1: occlusion)
-__device__ __forceinline__ void tail_lists(const rtk::Emit& e, int last_kind, rtk::RayRec* l0, rtk::RayRec* l1, int* nl)
+__device__ __forceinline__ void tail_lists(const rtk::Emit& e, int slot, int last_kind, rtk::RayRec* l0, rtk::RayRec* l1,
+                                           int* nl)
 {
     const int lane = lane_id();
     nl[0] = nl[1] = 0;
@@ -824,9 +825,7 @@ __device__ __forceinline__ void tail_lists(const rtk::Emit& e, int last_kind, rt
         const int l = k <= last_kind ? 0 : 1;
         if (want) {
             const int pos = nl[l] + __popcll(b & ((1ull << lane) - 1ull));
-            rtk::RayRec r = e.r[k];
-            r.d.w = rt_asfloat((rt_asuint(r.o.w) << 3) | (uint32_t)k);
-            (l ? l1 : l0)[pos] = r;
+            (l ? l1 : l0)[pos] = e.rec(k, slot, rt_asfloat(((uint32_t)slot << 3) | (uint32_t)k));
         }
         nl[l] += __popcll(b);
     }
@@ -844,7 +843,7 @@ __device__ __noinline__ int tail_step(const rtk::WaveView& W, int my, int last_k
     e.heavy = false;
     if (my >= 0) rtk::path_step(W, my, e, ps);
     int nl[2];
-    tail_lists(e, last_kind, l0, l1, nl);
+    tail_lists(e, my, last_kind, l0, l1, nl);
     return (e.active ? 1 : 0) | (nl[0] << 1) | (nl[1] << 11);
 }
 // k_tail's inline exact walk (a query the quad walk cannot settle: ~1e-6 of them), kept

@@ -36,7 +36,6 @@ enum PathFlag : uint32_t {
     PF_BL = 16u,         // BRDF->light ray emitted
     PF_ESH = 32u,        // env shadow ray emitted
     PF_BENV = 64u,       // BRDF->env ray emitted
-    PF_EMIT0 = 128u,     // bounce 0: add the material emission at resolve
     PF_CAM = 256u,       // the next sample's camera ray is in flight (next_camera)
 };
 #define RT_FLAG_BITS 12  // p_rd.w = flags | bounce << RT_FLAG_BITS
@@ -90,7 +89,6 @@ struct WaveView {
     float4_* q_blo;         // BRDF->light origin xyz (sphere hit normals)
     float4_* q_env;         // env candidate rgb
     float4_* q_benv;        // BRDF->env candidate rgb
-    float4_* q_em;          // emission rgb (bounce 0)
     float4_* q_thr;         // thr at the shaded bounce
     // query results
     float* r_cont_t;
@@ -156,7 +154,6 @@ inline size_t wave_carve(char* base, size_t n, WaveView& W)  // uses W.park_cap,
     W.q_blo = (float4_*)take(n * 16);
     W.q_env = (float4_*)take(n * 16);
     W.q_benv = (float4_*)take(n * 16);
-    W.q_em = (float4_*)take(n * 16);
     W.q_thr = (float4_*)take(n * 16);
     W.r_cont_t = (float*)take(n * 4);
     W.r_cont_k = (int32_t*)take(n * 4);
@@ -192,18 +189,27 @@ RT_HD float4_ f4(Col c, float w) { return float4_{c.r, c.g, c.b, w}; }
 RT_HD V3 v3of(const float4_& f) { return v3(f.x, f.y, f.z); }
 RT_HD Col colof(const float4_& f) { return Col{f.x, f.y, f.z}; }
 
-// What one path step hands to the queues.
+// What one path step hands to the queues: per kind the ray (the slot goes into the
+// queue record when it is written, rec()).
 struct Emit {
-    RayRec r[RK_COUNT];
+    V3 o[RK_COUNT], d[RK_COUNT];
     uint32_t mask;  // bit k: a ray of kind k
     bool active;    // the path stays in flight
     bool heavy;     // the rays go to the heavy class (WaveView::qh)
+    RT_HD RayRec rec(int kind, int slot, float dw = 0.0f) const
+    {
+        RayRec r;
+        r.o = float4_{o[kind].x, o[kind].y, o[kind].z, rt_asfloat((uint32_t)slot)};
+        r.d = float4_{d[kind].x, d[kind].y, d[kind].z, dw};
+        return r;
+    }
 };
 
 RT_HD void emit(Emit& e, int kind, int slot, V3 o, V3 d)
 {
-    e.r[kind].o = f4(o, rt_asfloat((uint32_t)slot));
-    e.r[kind].d = f4(d, 0.0f);
+    (void)slot;  // (the step's own slot: written with the record)
+    e.o[kind] = o;
+    e.d[kind] = d;
     e.mask |= 1u << kind;
 }
 
@@ -588,10 +594,9 @@ RT_HD void shade(const WaveView& W, int p, PathReg& P, const Hit& h, Emit& e, St
     float bpdf;
     V3 dir = v3(0.0f, 0.0f, 0.0f);
     Col brdf = ct_sample(m, neg(rd), h.n, dir, bpdf, P.rng);
-    if (P.bounce == 0) {
-        fl |= PF_EMIT0;
-        W.q_em[p] = f4(m.emission, 0.0f);
-    }
+    // bounce 0: sample_color += material.emission (:126) — sc is still the sample start's 0 and
+    // nothing else adds to it before this bounce's resolve, so the same addition happens here
+    if (P.bounce == 0) P.sc = cadd(P.sc, m.emission);
     W.q_thr[p] = f4(P.thr, 0.0f);
     if ((brdf.r == 0.0f && brdf.g == 0.0f && brdf.b == 0.0f) || bpdf < 1.0e-8f || rt_isinf(bpdf)) {
         fl |= PF_END;  // `break` after this bounce's light is added
@@ -680,15 +685,15 @@ RT_HD void resolve(const WaveView& W, int p, PathReg& P, const ResolveRec& R, St
     if ((fl & PF_BENV) && !r_benv) brdf_sample = colof(q_benv);
     const Col lr = cadd(light, bmis);
     const Col er = cadd(brdf_sample, env_sample);
-    if (fl & PF_EMIT0) P.sc = cadd(P.sc, colof(W.q_em[p]));
     P.sc = cadd(P.sc, cmul(cadd(lr, er), colof(q_thr)));
 }
 
 // One iteration of path slot p: resolve the bounce shaded last iteration,
 // consume the continuation query, shade the new hit or end the sample; a sample
 // that ends goes on with the next one: its camera answer, when it was traced ahead
-// (next_camera), is consumed in the same step (shaded, or that sample ends too), else
-// its camera ray is cast. Fills `e` with the rays for the next trace.
+// (next_camera), is consumed in the same step (shaded, or that sample ends too and
+// the next camera ray is cast), else its camera ray is cast. Fills `e` with the rays
+// for the next trace.
 RT_HD void path_step(const WaveView& W, int p, Emit& e, Stats* st)
 {
     e.mask = 0;
@@ -722,44 +727,44 @@ RT_HD void path_step(const WaveView& W, int p, Emit& e, Stats* st)
         tr2 = W.S.tri4[3 * tk + 2];
     }
     if (fl0 & PF_AUX) resolve(W, p, P, R, st);
-    bool end = (P.flags & PF_END) != 0;
+    // the hit this step shades, if any: the continuation's, or else (the sample over) the
+    // next sample's camera hit traced ahead; shade() is called from one place only (its
+    // registers, not twice its code)
+    bool end = (P.flags & PF_END) != 0, fin_changed = false, do_shade = false;
+    Hit h;
     if (P.flags & PF_CONT) {
-        const float t = cont_t;
-        Hit h;
-        if (hit_from_rec(W.S, P.ro, P.rd, t, cont_k, tr0, tr1, tr2, h)) {
-            shade(W, p, P, h, e, st);
-            store_path(W, p, P, false);
-            return;
+        if (hit_from_rec(W.S, P.ro, P.rd, cont_t, cont_k, tr0, tr1, tr2, h)) {
+            do_shade = true;
+        } else {
+            // MISSED (:143-160): the next loop iteration adds the sky only when
+            // it is bounce 1, i.e. the camera ray missed; then `break`.
+            if (P.bounce == 0 && W.bounces >= 2) P.sc = cadd(P.sc, cmul(env_from_dir(W.S, P.rd, st), P.thr));
+            end = true;
         }
-        // MISSED (:143-160): the next loop iteration adds the sky only when
-        // it is bounce 1, i.e. the camera ray missed; then `break`.
-        if (P.bounce == 0 && W.bounces >= 2) P.sc = cadd(P.sc, cmul(env_from_dir(W.S, P.rd, st), P.thr));
-        end = true;
     }
-    bool ahead = (fl0 & PF_CAM) != 0;  // the next sample's camera answer is here
-    while (end) {
+    if (end) {
+        fin_changed = true;
         P.fin = cadd(P.fin, P.sc);
-        if (++P.sample == W.spp) {
-            e.active = false;
-            break;
+        bool start = ++P.sample < W.spp;
+        if (start && (fl0 & PF_CAM)) {  // the next sample, its camera ray traced ahead: its answer now
+            begin_sample_ahead(W, p, P);
+            if (hit_from_rec(W.S, P.ro, P.rd, cam_t, cam_k, tr0, tr1, tr2, h)) {
+                do_shade = true;
+                start = false;
+            } else {  // (bounce 0 missed: the sky, and that sample is over too)
+                if (W.bounces >= 2) P.sc = cadd(P.sc, cmul(env_from_dir(W.S, P.rd, st), P.thr));
+                P.fin = cadd(P.fin, P.sc);
+                start = ++P.sample < W.spp;
+            }
         }
-        if (!ahead) {
-            e.active = start_sample(W, p, P, e);
-            break;
-        }
-        // the next sample, its camera ray traced ahead: consume its answer now
-        ahead = false;
-        begin_sample_ahead(W, p, P);
-        Hit h;
-        if (hit_from_rec(W.S, P.ro, P.rd, cam_t, cam_k, tr0, tr1, tr2, h)) {
-            shade(W, p, P, h, e, st);
-            store_path(W, p, P, true);
-            return;
-        }
-        if (W.bounces >= 2) P.sc = cadd(P.sc, cmul(env_from_dir(W.S, P.rd, st), P.thr));  // (bounce 0 missed)
+        if (!do_shade) e.active = start && start_sample(W, p, P, e);
     }
-    if (!e.active) finish_pixel(W, p, P);
-    store_path(W, p, P, end);
+    if (do_shade) {
+        shade(W, p, P, h, e, st);
+    } else if (!e.active) {
+        finish_pixel(W, p, P);
+    }
+    store_path(W, p, P, fin_changed);
 }
 
 // --------------------------------------------------------------- queries
