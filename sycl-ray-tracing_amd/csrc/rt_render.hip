@@ -1440,8 +1440,12 @@ int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounces, cons
     int tail_p = 5;  // (5 paths: 15 queries, one pass of the wave's 16 quads; sweep 2-6 within 1 %)
     if (const char* e = getenv("RT_TAIL_PATHS")) tail_p = std::min(RT_TAIL_MAXP, std::max(0, atoi(e)));
     const int tail_blocks = dev_cus * RT_TAIL_OCC;  // one grid-fill of k_tail
-    long tail_max = (long)tail_blocks * 4 * tail_p / nl;  // (one grid-fill's pool per lane)
-    if (const char* e = getenv("RT_TAIL_ENTER")) tail_max = (long)(tail_max * atof(e));  // (sweeps)
+    // a lane enters the tail kernel at 0.7 of one grid-fill's pool: with camera-ahead steps
+    // (r03, RT_TAIL_ENTER = 1 / 0.8 / 0.6 / 0.4): cfg2 870-874 / 886-888 / 888-894 / 879-882
+    // Msamples/s, cfg4 8-way shard 380 / 374 / 378 / 380 ms
+    double tail_enter = 0.7;
+    if (const char* e = getenv("RT_TAIL_ENTER")) tail_enter = atof(e);  // (sweeps)
+    const long tail_max = (long)(tail_enter * tail_blocks * 4 * tail_p / nl);
     if (nl > 1) {
         HIPCHK(c, hipEventRecord(b->ev_fork, s));
         for (int l = 1; l < nl; l++) HIPCHK(c, hipStreamWaitEvent(b->ls[l], b->ev_fork, 0));
