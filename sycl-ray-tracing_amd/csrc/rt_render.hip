@@ -718,6 +718,13 @@ __device__ __forceinline__ void trace_stream(const rtk::WaveView& W, const RtSce
                 active = false;
                 // a long walk: the path's next rays go to the heavy class (head of the next streams)
                 if (W.r_heavy && sub == 0 && q.calls >= W.heavy_calls) W.r_heavy[target >> 3] = 1;
+                if (STATS && W.iterq && sub == 0 && W.iter < RT_MAX_TIMED_ITERS) {
+                    // (RT_ITER_LOG: the launch's longest walk in quad_visit calls per role, and
+                    // how many walks took more than 8)
+                    int32_t* q2 = W.iterq + 2 * RT_MAX_TIMED_ITERS + 4 * W.iter;
+                    atomicMax(q2 + (ANY ? 1 : 0), q.calls);
+                    if (q.calls > 8) atomicAdd(q2 + 2, 1);
+                }
                 float t = 0.0f;
                 int k = 0;
                 if (res > 0 && !ANY && !rtk::quad_closest_answer(S, q, sub, t, k, ps)) res = -1;

@@ -67,9 +67,10 @@ def main():
         out["bands"].append({"live": f"({lo}, {hi}]", "iters": int(sel.sum()),
                              "trace_ms": round(float(ms[sel, 1].sum()), 2), "step_ms": round(float(ms[sel, 2].sum()), 2),
                              "queries": int(cnt[:n_it][sel, 1].sum()),
-                             # the longest walk of each launch (node visits, closest / occlusion), band mean
+                             # the longest walk of each launch (quad_visit calls, closest / occlusion), band mean
                              "max_visits_c": round(float(cnt[:n_it][sel, 3].mean()), 1) if sel.any() else 0.0,
                              "max_visits_a": round(float(cnt[:n_it][sel, 4].mean()), 1) if sel.any() else 0.0,
+                             "walks_over_8_calls": int(cnt[:n_it][sel, 5].sum()),
                              "us_per_trace": round(float(ms[sel, 1].sum()) * 1e3 / max(1, int(sel.sum())), 1)})
     # the tail launch: rounds of its longest pool loop, 100 MHz ticks / 16 in steps and in walks (summed over waves)
     ti = int(cnt.shape[0]) - 1
