@@ -1,11 +1,12 @@
 """Per-rank render time of a row shard, on one GPU (multi-GPU scaling probe).
 
-Renders rank 0's share (rows y % N == 0) of a config for N in --worlds and
-prints the time per render, the per-GPU rate and the strong-scaling
-efficiency it implies (T_1 / (N * T_N)); the RCCL gather is not included
-(it is ~0.1 ms at 1080p).
+Renders the shares (rows y % N == r) of a config for N in --worlds — every rank's
+with --all-ranks, else rank 0's — and prints the time per render, the per-GPU rate
+and the strong-scaling efficiency it implies, T_1 / (N * max_r T_N,r) (the slowest
+rank sets the frame); the RCCL gather is not included (it is ~0.1 ms at 1080p,
+DESIGN.md §6).
 
-  python tools/shard_probe.py [--config cfg2] [--worlds 1,2,4,8] [--reps 2]
+  python tools/shard_probe.py [--config cfg2] [--worlds 1,2,4,8] [--reps 2] [--all-ranks]
 """
 from __future__ import annotations
 
@@ -25,6 +26,7 @@ def main():
     ap.add_argument("--config", default="cfg2")
     ap.add_argument("--worlds", default="1,2,4,8")
     ap.add_argument("--reps", type=int, default=2)
+    ap.add_argument("--all-ranks", action="store_true")
     args = ap.parse_args()
     import torch
 
@@ -43,20 +45,27 @@ def main():
     out = {"config": args.config, "desc": desc, "runs": []}
     t1 = None
     for n in [int(x) for x in args.worlds.split(",")]:
-        fr = ShardedFrame(rk, 0, n, device=dev)
-        fr.render(stream)
-        torch.cuda.synchronize(dev)
-        ts = []
-        for _ in range(args.reps):
-            t0 = time.perf_counter()
+        per_rank = []
+        for rank in (range(n) if args.all_ranks else [0]):
+            fr = ShardedFrame(rk, rank, n, device=dev)
             fr.render(stream)
             torch.cuda.synchronize(dev)
-            ts.append(time.perf_counter() - t0)
-        t = min(ts)
+            ts = []
+            for _ in range(args.reps):
+                t0 = time.perf_counter()
+                fr.render(stream)
+                torch.cuda.synchronize(dev)
+                ts.append(time.perf_counter() - t0)
+            per_rank.append((min(ts), fr.rows, rk.last_iterations()))
+        t = max(p[0] for p in per_rank)
         t1 = t if n == 1 else t1
-        samples = fr.rows * W * spp
-        r = {"world": n, "rows": fr.rows, "ms": round(t * 1e3, 2), "iters": rk.last_iterations(),
+        rows = per_rank[0][1]
+        samples = rows * W * spp
+        r = {"world": n, "rows": rows, "ms": round(t * 1e3, 2), "iters": max(p[2] for p in per_rank),
              "msamples_per_s_per_gpu": round(samples / t / 1e6, 1)}
+        if len(per_rank) > 1:
+            r["ms_per_rank"] = [round(p[0] * 1e3, 2) for p in per_rank]
+            r["slowest_rank"] = int(max(range(len(per_rank)), key=lambda i: per_rank[i][0]))
         if t1 is not None:
             r["strong_eff_vs_1"] = round(t1 / (n * t), 3)
         out["runs"].append(r)
