@@ -107,20 +107,20 @@ def _step_bytes(g) -> float:
 
 
 # Wavefront step model: what a path step must read besides the scene
-# records above. Per step (one continuation result consumed): the slot's 4 state
-# records (64 B), its result (8 B), live-list entry and wait count (8 B); per shaded
-# bounce: the hit triangle (48 B) and the pending throughput (16 B); per occlusion
-# query: its candidate (16 B) and answer (1 B); per sample: the fin record (16 B).
-# Exact for scenes without emissive triangles (cfg2-cfg5: every closest query is a
-# continuation and every material load a shade).
-SLOT_BYTES = {"step": 80, "shade": 64, "occ": 17, "sample": 16}
+# records above. Per step (the `steps` counter): the slot's 4 state records (64 B), its
+# continuation and camera-ahead results (16 B), live-list entry and wait count (8 B);
+# per shaded bounce: the hit triangle (48 B) and the pending throughput (16 B); per
+# occlusion query: its candidate (16 B) and answer (1 B); per sample: the fin record
+# (16 B). Exact for scenes without emissive triangles (cfg2-cfg5: every material load
+# is a shade).
+SLOT_BYTES = {"step": 88, "shade": 64, "occ": 17, "sample": 16}
 
 
 def step_model_bytes(st: dict, samples: float) -> dict:
     rest = lambda k: st[k] - st.get("tail_" + k, 0)  # noqa: E731
     scene = _step_bytes(rest)
     tail_frac = 1.0 - rest("rays") / max(st["rays"], 1)
-    slot = (SLOT_BYTES["step"] * rest("rays") + SLOT_BYTES["shade"] * rest("mat") +
+    slot = (SLOT_BYTES["step"] * rest("steps") + SLOT_BYTES["shade"] * rest("mat") +
             SLOT_BYTES["occ"] * rest("any_rays") + SLOT_BYTES["sample"] * samples * (1.0 - tail_frac))
     return {"scene": scene, "slot": slot}
 
@@ -554,6 +554,10 @@ def main():
         achieved = algo / (avg_ms * 1e-3) / 1e9
         roofline = {"bound": "hbm", "kernel": "k_trace", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                    "byte_model": "records a query must read (bench.py BYTES): 32 B per search-BVH box test (one "
+                                  "child record), 48 B per triangle test, 64 B per octree verification slab test, "
+                                  "40 B per query (queue ray + result); box tests counted as executed, incl. the "
+                                  "paired occlusion trips' stack-top node",
                     "traffic": load_traffic(f"{args.config}_1lane") if (n_gpus == 1 and not args.sim_world) else None,
                     "measured": "1-lane render after the timed steps (one stream: launches do not overlap); "
                                 "HIP events around each launch",

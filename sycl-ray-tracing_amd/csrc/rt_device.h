@@ -131,5 +131,6 @@ enum {
     RT_STAT_REFILLS,      // k_trace stream: refill rounds of the waves
     RT_STAT_DRAIN_SLOTS,  // k_trace stream: the WAVE_SLOTS spent after the wave's stream ran out
     RT_STAT_DRAIN_VISITS, // ... and the QUAD_VISITS among them
+    RT_STAT_STEPS,        // path steps (rt_wave.h path_step calls that were not waiting on a parked walk)
     RT_STAT_COUNT
 };

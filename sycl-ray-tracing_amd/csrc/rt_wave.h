@@ -709,6 +709,7 @@ RT_HD void path_step(const WaveView& W, int p, Emit& e, Stats* st)
     const float cam_t = W.r_cam_t[p];  // (read only with PF_CAM)
     const int cam_k = W.r_cam_k[p];
     if (park != 0) return;  // a query of this path is parked: wait
+    if (st) st->c[RT_STAT_STEPS]++;
     if (heavy) {  // its last walk was long: this step's rays head the next streams
         e.heavy = true;
         W.r_heavy[p] = 0;

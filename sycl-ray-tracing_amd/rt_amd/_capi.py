@@ -80,7 +80,8 @@ _SIGS = {
 }
 
 STAT_NAMES = ["rays", "vol", "tri", "leaf", "mat", "env", "cdf", "heap_slow", "any_rays", "any_vol", "any_tri",
-              "any_leaf", "verify", "fallback", "quad_visits", "wave_slots", "refills", "drain_slots", "drain_visits"]
+              "any_leaf", "verify", "fallback", "quad_visits", "wave_slots", "refills", "drain_slots", "drain_visits",
+              "steps"]
 
 _libs: dict = {}
 
