@@ -1690,6 +1690,19 @@ int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounces, cons
                     }
                 }
         if (lf) fclose(lf);
+        // RT_TIMELINE=file: every lane's launches on one clock (ms from lane 0's first
+        // k_trace): lane, iteration, k_trace start, k_trace end = k_step start, k_step end,
+        // 1 for the tail kernel (tools/timeline.py)
+        if (const char* tl = getenv("RT_TIMELINE"))
+            if (FILE* f = fopen(tl, "w")) {
+                for (int l = 0; l < nl; l++)
+                    for (int i = 0; i < L[l].it && i < RT_MAX_TIMED_ITERS; i++) {
+                        float t[3];
+                        for (int k = 0; k < 3; k++) HIPCHK(c, hipEventElapsedTime(&t[k], L[0].tev[0][0], L[l].tev[k][i]));
+                        fprintf(f, "%d %d %.4f %.4f %.4f %d\n", l, i, t[0], t[1], t[2], i == L[l].tail_iter ? 1 : 0);
+                    }
+                fclose(f);
+            }
     }
     return RT_OK;
 }
