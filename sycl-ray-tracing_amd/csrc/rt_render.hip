@@ -670,8 +670,7 @@ __device__ __forceinline__ void trace_stream(const rtk::WaveView& W, const RtSce
     bool exhausted = wg * 16 >= total;  // (uniform)
     bool active = false;
     uint32_t target = 0;
-    rtk::QState q;
-    rtk::RayRec r;
+    rtk::QState q;  // (its ray is the query's: a fallback record is rebuilt from q.o, q.d and target)
     for (;;) {
         const unsigned long long bidle = __ballot(!active && sub == 0);
         if (!exhausted && (__popcll(bidle) >= RT_TRACE_REFILL || bidle == 0x1111111111111111ull)) {
@@ -680,7 +679,7 @@ __device__ __forceinline__ void trace_stream(const rtk::WaveView& W, const RtSce
                 const int idx = (wg + (j >> 4) * wn) * 16 + (j & 15);
                 if (idx < total) {
                     int kind;
-                    r = queue_item_at(W, s_pre, first + idx, kind);
+                    rtk::RayRec r = queue_item_at(W, s_pre, first + idx, kind);
                     target = (rt_asuint(r.o.w) << 3) | (uint32_t)kind;
                     if (forced_fallback(W, r.o, r.d)) {
                         if (sub == 0) {
@@ -734,9 +733,9 @@ __device__ __forceinline__ void trace_stream(const rtk::WaveView& W, const RtSce
                             rtk::finish_any(W, target, q.h.k == 1);
                         else
                             rtk::finish_closest(W, target, q.o, q.d, t, k);
-                    } else {  // the exact walk answers it (k_step(i))
-                        r.d.w = rt_asfloat(target & 7u);
-                        fbl[atomicAdd(fbn, 1)] = r;
+                    } else {  // the exact walk answers it (k_step(i)); the queue record again (o.w: slot)
+                        fbl[atomicAdd(fbn, 1)] = rtk::RayRec{rtk::f4(q.o, rt_asfloat(target >> 3)),
+                                                             rtk::f4(q.d, rt_asfloat(target & 7u))};
                         atomicAdd(&W.r_park[target >> 3], 1);
                     }
                 }
@@ -1444,13 +1443,18 @@ int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounces, cons
     if (const char* e = getenv("RT_HEAVY")) heavy_calls = std::max(0, atoi(e));
     int spec_cam = 1;  // the next sample's camera ray traced ahead (rt_wave.h next_camera); RT_SPEC_CAM=0: off
     if (const char* e = getenv("RT_SPEC_CAM")) spec_cam = atoi(e) != 0;
-    int tail_p = 5;  // (5 paths: 15 queries, one pass of the wave's 16 quads; sweep 2-6 within 1 %)
+    // k_tail paths per wave: a round waits for the slowest walk of the wave's ~3 P queries, so
+    // fewer paths per wave move each chain faster. With the entry held at the same live count
+    // (r03, P x RT_TAIL_ENTER = 3.5): P = 5 / 3 / 2 / 1 -> cfg2 886-893 / 892-896 / 897-901 /
+    // 887-890 Msamples/s, cfg4 8-way shard (slowest rank) 401 / - / 390 / 405 ms
+    int tail_p = 2;
     if (const char* e = getenv("RT_TAIL_PATHS")) tail_p = std::min(RT_TAIL_MAXP, std::max(0, atoi(e)));
     const int tail_blocks = dev_cus * RT_TAIL_OCC;  // one grid-fill of k_tail
-    // a lane enters the tail kernel at 0.7 of one grid-fill's pool: with camera-ahead steps
-    // (r03, RT_TAIL_ENTER = 1 / 0.8 / 0.6 / 0.4): cfg2 870-874 / 886-888 / 888-894 / 879-882
-    // Msamples/s, cfg4 8-way shard 380 / 374 / 378 / 380 ms
-    double tail_enter = 0.7;
+    // a lane enters the tail kernel at 2x one grid-fill's pool (the waves refill from the live
+    // list): with 2 paths per wave, RT_TAIL_ENTER = 1.4 / 1.75 / 2.2 / 2.8 -> cfg2 888-897 /
+    // 891-898 / 893-897 / 874-879 Msamples/s (5 paths at 0.7: 888-892), cfg4 8-way shard
+    // 393.5 / 389.6 / 393.1 / - ms (profiles/r03_tail_paths_ab.json)
+    double tail_enter = 2.0;
     if (const char* e = getenv("RT_TAIL_ENTER")) tail_enter = atof(e);  // (sweeps)
     const long tail_max = (long)(tail_enter * tail_blocks * 4 * tail_p / nl);
     if (nl > 1) {
