@@ -590,10 +590,17 @@ def main():
 
     cpu, parity = None, None
     if rank == 0 and world == 1 and n_gpus == 1 and not args.sim_world and not args.no_cpu_baseline and full is not None:
-        threads = int(os.environ.get("OMP_NUM_THREADS", 0)) or len(os.sched_getaffinity(0))
-        threads = min(threads, len(os.sched_getaffinity(0)))
+        omp = os.environ.get("OMP_NUM_THREADS")
+        aff = len(os.sched_getaffinity(0))
+        threads = min(int(omp or 0) or aff, aff)
         gpu_frame = full.cpu().numpy()
         cpu, parity, ref = cpu_baseline(P, sky, cam17, W, H, spp, nb, gpu_frame, threads, args.cpu_row_step)
+        # where the core count comes from: the box sets OMP_NUM_THREADS (its CPU share), capped
+        # by this process's affinity mask; the model string names the whole socket
+        cpu["cores_source"] = (f"OMP_NUM_THREADS={omp} (the host's CPU share for this job) capped by the process's "
+                               f"CPU affinity ({aff} CPUs, os.sched_getaffinity); os.cpu_count() = {os.cpu_count()}"
+                               if omp else f"the process's CPU affinity ({aff} CPUs, os.sched_getaffinity); "
+                                           f"os.cpu_count() = {os.cpu_count()}")
         if roofline is not None:
             roofline.update(ref)
             # the reference walk's bytes at this throughput: above 8 TB/s, because the search BVH + octree
