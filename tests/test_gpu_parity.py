@@ -360,3 +360,40 @@ def test_gpu_full_rows_at_256spp_match_oracle(name, off, stride, manifest, camer
     e["px"] = np.stack([xs.ravel(), ys.ravel()], 1).astype(np.int32)
     want = rt_cases.run_oracle(e, cameras)
     assert_parity(got.reshape(-1, 4), want, min_bitwise=1.0)
+
+
+def test_gpu_cfg4_full_frame_rows_match_oracle(manifest, cameras):
+    """Cfg4 (4K x 256 spp x 8, the 8-GPU config) rendered as one whole frame on the GPU
+    (the 1-GPU leg of bench.py's strong_cfg4): four rows spread over the frame against
+    the oracle, bitwise, and every golden pixel of the compiled reference."""
+    e = rt_cases.golden_case("cfg4_dragon4k", manifest)
+    rk, fb = rt_cases.make_kernel(e, cameras, hostsim=False)
+    rk.render()
+    rows = np.arange(137, e["H"], 540)
+    xs, ys = np.meshgrid(np.arange(e["W"]), rows)
+    o = dict(e)
+    o["px"] = np.stack([xs.ravel(), ys.ravel()], 1).astype(np.int32)
+    want = rt_cases.run_oracle(o, cameras)
+    assert_parity(fb.pixels[rows].reshape(-1, 4), want, min_bitwise=1.0)
+    assert_parity(fb.pixels[e["px"][:, 1], e["px"][:, 0]], e["expected"], min_bitwise=1.0)
+
+
+@pytest.mark.parametrize("variant", ["cfg5_sweep_m0_r0", "cfg5_sweep_m3_r3"])
+def test_gpu_cfg5_variant_row_matches_oracle(variant, manifest, cameras):
+    """Two cfg5 sweep variants at their full 1024 spp (the smoothest dielectric and the
+    roughest metal of the grid): a whole image row through the dragon, rendered as
+    a row shard on the GPU, against the oracle with the variant's material table."""
+    from hip_mem import DeviceBuffer
+    e = rt_cases.golden_case(variant, manifest)
+    rk, _ = rt_cases.make_kernel(e, cameras, hostsim=False)
+    off, stride = 700, e["H"]  # (one row)
+    init = np.zeros((1, e["W"], 4), np.float32)
+    init[..., 3] = 1.0
+    buf = DeviceBuffer(init.nbytes)
+    buf.upload(init)
+    rk.render_device(buf.ptr, off, stride, None)
+    got = buf.download(init.shape, np.float32)
+    o = dict(e)
+    o["px"] = np.stack([np.arange(e["W"]), np.full(e["W"], off)], 1).astype(np.int32)
+    want = rt_cases.run_oracle(o, cameras)
+    assert_parity(got.reshape(-1, 4), want, min_bitwise=1.0)
