@@ -265,19 +265,22 @@ def test_gpu_slab_division_exact():
 
 def test_gpu_schedules_bit_identical(monkeypatch):
     """The frame does not depend on the schedule: 1-4 wavefront lanes, the
-    tail kernel on or off, row shards split across lanes (framebuffer row
-    pitch) and k_trace's heavy class (off, every walk heavy, the default) all
-    give the same bits as one lane without the tail kernel."""
+    tail kernel on or off (1-8 paths per wave, entered at once or late), row
+    shards split across lanes (framebuffer row pitch), k_trace's heavy class
+    (off, every walk heavy, the default) and the camera ray traced ahead or not
+    all give the same bits as one lane without the tail kernel."""
     import scenes
     from hip_mem import DeviceBuffer
     P = rt_amd.parse_obj(scenes.scene_path("dragon_small"))
     sky = scenes.make_sky("L")
     W, H, spp, nb = 640, 480, 2, 8
 
-    def render(lanes, tail, off=0, stride=1, heavy=6):
+    def render(lanes, tail, off=0, stride=1, heavy=6, enter=2.0, spec_cam=1):
         monkeypatch.setenv("RT_LANES", str(lanes))
         monkeypatch.setenv("RT_TAIL_PATHS", str(tail))
         monkeypatch.setenv("RT_HEAVY", str(heavy))
+        monkeypatch.setenv("RT_TAIL_ENTER", str(enter))
+        monkeypatch.setenv("RT_SPEC_CAM", str(spec_cam))
         rk = rt_amd.RenderKernel(W, H, spp, nb, rt_amd.Image(1, 1), P.triangles, P.materials,
                                  P.emissive_triangle_indices, P.material_indices, None, rt_amd.BVH(P.triangles),
                                  rt_amd.Image.from_rgb(sky), None, device=0)
@@ -301,6 +304,15 @@ def test_gpu_schedules_bit_identical(monkeypatch):
     for heavy in (0, 1):  # heavy class off / every path's rays in the heavy shards
         got = render(3, 4, heavy=heavy)
         np.testing.assert_array_equal(got.view(np.uint32), base.view(np.uint32), err_msg=f"heavy={heavy}")
+    # the tail kernel entered at once (it takes nearly every path, its waves refilling from
+    # the live list) with 1 and 2 paths per wave; the next camera ray not traced ahead
+    for lanes, tail, enter in ((3, 1, 1000.0), (2, 2, 1000.0), (1, 2, 1000.0)):
+        got = render(lanes, tail, enter=enter)
+        np.testing.assert_array_equal(got.view(np.uint32), base.view(np.uint32),
+                                      err_msg=f"lanes={lanes} tail={tail} enter={enter}")
+    for lanes, tail in ((1, 0), (3, 2)):
+        got = render(lanes, tail, spec_cam=0)
+        np.testing.assert_array_equal(got.view(np.uint32), base.view(np.uint32), err_msg=f"spec_cam=0 lanes={lanes}")
 
 
 @pytest.mark.gpu
