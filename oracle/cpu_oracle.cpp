@@ -68,8 +68,10 @@ inline float luminance(Col c) { return 0.3086f * c.r + 0.6094f * c.g + 0.0820f *
 // ------------------------------------------------- include/xorshift.h
 struct Rng {  // xorshift.h:10-31
     uint32_t a;
+    uint32_t draws = 0;  // (analysis only: draws so far, oracle_render_log)
     float operator()()
     {
+        draws++;
         uint32_t x = a;
         x ^= x << 13;
         x ^= x >> 17;
@@ -668,13 +670,15 @@ Col sample_lights(const Ctx& C, const Ray& ray, const Hit& h, const Mat& m, Rng&
     return light + bmis;
 }
 
-void trace_pixel(const Ctx& C, int x, int y, float* fb)  // render_kernel.cpp:75-181
+// draws_log (analysis only, oracle_render_log): the RNG draws of each sample, spp entries
+void trace_pixel(const Ctx& C, int x, int y, float* fb, uint16_t* draws_log = nullptr)  // render_kernel.cpp:75-181
 {
     const Scene& S = C.S;
     Rng rng{(uint32_t)(31 + x * y * C.spp)};
     for (int i = 0; i < 10; i++) rng();
     Col fin = col(0.0f);
     for (int s = 0; s < C.spp; s++) {
+        const uint32_t d0 = rng.draws;
         float xj = (x + 0.5f) + rng() - 1.0f;
         float yj = (y + 0.5f) + rng() - 1.0f;
         Ray ray = camera_ray(C, xj, yj);
@@ -708,6 +712,7 @@ void trace_pixel(const Ctx& C, int x, int y, float* fb)  // render_kernel.cpp:75
                 break;
         }
         fin = fin + sc;
+        if (draws_log) draws_log[s] = (uint16_t)(rng.draws - d0);
     }
     float k = (float)C.spp;
     fin.r /= k;
@@ -892,6 +897,24 @@ double oracle_render(void* s, const float* view16, float fov_dist, int W, int H,
         counters[4] = tot.leaf_visits;
     }
     return t1 - t0;
+}
+
+// Analysis only (tools/chain_model.py): oracle_render over a pixel list, logging each
+// sample's RNG draw count into draws_log[n][spp] — the per-pixel sample chain the GPU
+// wavefront walks in order.
+void oracle_render_log(void* s, const float* view16, float fov_dist, int W, int H, int spp, int bounces,
+                       const int* px, long n, float* fb, uint16_t* draws_log)
+{
+    const Scene& S = *(Scene*)s;
+    Cam cam;
+    std::memcpy(cam.m, view16, 64);
+    cam.fov_dist = fov_dist;
+#pragma omp parallel
+    {
+        Ctx C{S, cam, W, H, spp, bounces, nullptr, nullptr};
+#pragma omp for schedule(dynamic, 16)
+        for (long i = 0; i < n; i++) trace_pixel(C, px[2 * i], px[2 * i + 1], fb, draws_log + (size_t)i * spp);
+    }
 }
 
 }  // extern "C"

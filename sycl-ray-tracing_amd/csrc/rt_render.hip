@@ -154,6 +154,7 @@ struct Backend {
     DevBuf iterq;     // stats renders: per-iteration {queries, live slots} (RT_ITER_LOG)
     DevBuf wave[RT_MAX_LANES];      // per lane: path state, pending records, results, queues, lists
     DevBuf counters[RT_MAX_LANES];  // per lane: C_COUNT int32
+    DevBuf aq[RT_MAX_LANES];        // per lane: k_async's queues (AsyncQ)
     DevBuf xy;        // pixel list (rt_render_pixels)
     DevBuf fb;        // host-fb staging
     int32_t* h_act[RT_MAX_LANES] = {};     // per lane, pinned: live-slot counters (sharded) + 8 fallback counters
@@ -1013,6 +1014,330 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TAIL_OCC
     flush_stats<STATS>(st, stats + RT_STAT_COUNT);  // (the tail kernel's share, for per-kernel byte counts)
 }
 
+// ------------------------------------------------------------- async kernel
+// k_async: the tail kernel without a path's wave. Once the live count is low, an iteration
+// of the wavefront costs its slowest walk plus a step launch however few paths it carries,
+// and k_tail's waves own their paths, so a path's round waits for the walks of the other
+// paths of its wave. Here paths and queries live in two global queues:
+//   RQ  ready paths (every query of the last step answered): a lane takes one and steps it,
+//       and the step's rays go to the QQ, with the path's pend count set to their number
+//       (a path with no rays goes straight back to the RQ, a finished path is counted);
+//   QQ  queries: an idle quad takes one and walks it (rt_quad.h quad_visit, the exact octree
+//       walk inline when the quad walk cannot settle it); the walk that answers a path's
+//       last query puts the path in the RQ.
+// Every wave alternates: step the ready paths its lanes hold, then a few walk trips. No
+// wave ever blocks on another: queue entries are taken by ticket (position) and a lane or
+// quad whose entry is not written yet simply checks again next loop, so progress needs no
+// particular set of waves resident. A path's step happens once all of its queries are
+// answered, exactly as in the wavefront, so the answers are bit-identical.
+// Memory order: a queue entry is published by a release store of its sequence word
+// (position + 1) after its record; the taker's acquire load of that word makes the
+// record, and everything the producer saw before it, visible (agent scope). The pend
+// count is decremented with acq_rel, so the step that follows a path's last answer sees
+// all of its answers.
+struct AsyncQ {
+    uint32_t* ctr;      // A_* counters, one 128-B line each
+    uint64_t* rq;       // ready paths: (position + 1) << 32 | slot, rq_mask + 1 entries
+    rtk::RayRec* qq;    // queries: the queue record (o.w = slot bits, d.w = target bits)
+    uint32_t* qq_seq;   // position + 1 once the record at that position is written
+    int32_t* pend;      // [n_slots] queries of the path's last step not answered yet
+    uint32_t rq_mask, qq_mask;
+    long long limit;    // wall_clock64 ticks (100 MHz) a wave may run before the launch gives up
+};
+enum { A_RQ_TAKE = 0, A_RQ_PUSH = 32, A_QQ_TAKE = 64, A_QQ_PUSH = 96, A_FIN = 128, A_ABORT = 160, A_COUNT = 192 };
+#ifndef RT_ASYNC_CALLS
+#define RT_ASYNC_CALLS 4  // quad_visit calls per walk phase before the wave looks for ready paths again
+#endif
+
+__device__ __forceinline__ uint32_t ld_relaxed(const uint32_t* p)
+{
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Wave-aggregated ticket: lanes with `want` get consecutive positions of the counter (converged call).
+__device__ __forceinline__ uint32_t take_tickets(uint32_t* ctr, unsigned long long b, int lane_bit_of_me)
+{
+    const int leader = __ffsll((long long)b) - 1;
+    uint32_t base = 0;
+    if (lane_id() == leader) base = atomicAdd(ctr, (uint32_t)__popcll(b));
+    base = __shfl(base, leader);
+    return base + (uint32_t)__popcll(b & ((1ull << lane_bit_of_me) - 1ull));
+}
+
+// The lanes with `want` put `slot` in the RQ (converged call). Positions below n0 are the
+// launch's initial live list.
+__device__ __forceinline__ void rq_push(const AsyncQ& A, uint32_t n0, bool want, int slot)
+{
+    const unsigned long long b = __ballot(want);
+    if (!b) return;
+    const uint32_t pos = n0 + take_tickets(A.ctr + A_RQ_PUSH, b, lane_id());
+    if (want)
+        __hip_atomic_store(A.rq + (pos & A.rq_mask), ((uint64_t)(pos + 1u) << 32) | (uint32_t)slot, __ATOMIC_RELEASE,
+                           __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Steps the paths the lanes hold (my >= 0), out of line like tail_step: the step's rays to
+// the QQ (pend = their number, set before any is published), a path without rays back to
+// the RQ, a finished path counted. Converged call.
+__device__ __noinline__ void async_step(const rtk::WaveView& W, const AsyncQ& A, int my, uint32_t n0, rtk::Stats* ps)
+{
+    rtk::Emit e;
+    e.mask = 0;
+    e.active = false;
+    e.heavy = false;
+    if (my >= 0) rtk::path_step(W, my, e, ps);
+    const int nr = __popc(e.mask);
+    if (my >= 0 && nr > 0) A.pend[my] = nr;
+    // one reservation for the wave's rays, in kind order
+    unsigned long long b[rtk::RK_COUNT];
+    int tot = 0;
+#pragma unroll
+    for (int k = 0; k < rtk::RK_COUNT; k++) {
+        b[k] = __ballot((e.mask >> k) & 1u);
+        tot += __popcll(b[k]);
+    }
+    if (tot > 0) {
+        uint32_t base = 0;
+        if (lane_id() == 0) base = atomicAdd(A.ctr + A_QQ_PUSH, (uint32_t)tot);
+        base = __shfl(base, 0);
+        const unsigned long long lt = (1ull << lane_id()) - 1ull;
+#pragma unroll
+        for (int k = 0; k < rtk::RK_COUNT; k++) {
+            if ((e.mask >> k) & 1u) {
+                const uint32_t pos = base + (uint32_t)__popcll(b[k] & lt);
+                A.qq[pos & A.qq_mask] = e.rec(k, my, rt_asfloat(((uint32_t)my << 3) | (uint32_t)k));
+                __hip_atomic_store(A.qq_seq + (pos & A.qq_mask), pos + 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            base += (uint32_t)__popcll(b[k]);
+        }
+    }
+    rq_push(A, n0, my >= 0 && e.active && nr == 0, my);
+    const unsigned long long bf = __ballot(my >= 0 && !e.active);
+    if (bf && lane_id() == 0) atomicAdd(A.ctr + A_FIN, (uint32_t)__popcll(bf));
+}
+
+// Block roles: every RT_ASYNC_STEP_EVERY-th block steps paths, the others walk queries, so a
+// query never waits behind a step of its walker's wave (a mixed wave, stepping and walking
+// in turn: cfg2 180 / 284 ms at entry 4096 / 16384 vs 146 for k_tail). A walker reads queue
+// records with L1-bypassing loads and its scene data is read-only, so only a stepper needs
+// the acquire fence (which invalidates its CU's L1) before it reads a path's state.
+#ifndef RT_ASYNC_STEP_EVERY
+#define RT_ASYNC_STEP_EVERY 4
+#endif
+template <bool STATS>
+__device__ __forceinline__ void async_stepper(const rtk::WaveView& W, const AsyncQ& A, uint32_t n0, int rank,
+                                              long long t_start, rtk::Stats* ps)
+{
+    const int lane = lane_id();
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    bool has_rt = false;
+    uint32_t rt = 0;  // this lane's RQ ticket
+    for (;;) {
+        uint32_t fin = 0, ab = 0, av = 0;
+        if (lane == 0) {
+            fin = ld_relaxed(A.ctr + A_FIN);
+            ab = ld_relaxed(A.ctr + A_ABORT);
+            av = n0 + ld_relaxed(A.ctr + A_RQ_PUSH) - ld_relaxed(A.ctr + A_RQ_TAKE);
+            if (wall_clock64() - t_start > A.limit) {
+                ab = 1;
+                __hip_atomic_store(A.ctr + A_ABORT, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+        fin = __shfl(fin, 0);
+        if (fin >= n0 || __shfl(ab, 0)) return;
+        const int rq_n = max(0, (int)__shfl(av, 0));
+        const bool holding = __any(has_rt);
+        if (!holding && rq_n == 0) {  // nothing here: leave once the live paths need fewer steppers
+            if (rank >= max(8, (int)((n0 - fin) / 32u))) return;
+            __builtin_amdgcn_s_sleep(2);
+            continue;
+        }
+        const unsigned long long bw = __ballot(!has_rt);
+        const bool sel = !has_rt && __popcll(bw & lt) < rq_n;
+        const unsigned long long bs = __ballot(sel);
+        if (bs) {
+            const uint32_t t = take_tickets(A.ctr + A_RQ_TAKE, bs, lane);
+            if (sel) rt = t, has_rt = true;
+        }
+        int my = -1;
+        if (has_rt) {
+            const uint64_t v = __hip_atomic_load(A.rq + (rt & A.rq_mask), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if ((uint32_t)(v >> 32) == rt + 1u) {
+                my = (int)(uint32_t)v;
+                has_rt = false;
+            }
+        }
+        if (__any(my >= 0)) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // (the path's state and answers)
+            async_step(W, A, my, n0, ps);
+        }
+    }
+}
+
+template <bool STATS>
+__device__ __forceinline__ void async_walker(const rtk::WaveView& W, const AsyncQ& A, uint32_t n0, int rank,
+                                             long long t_start, uint32_t* s_stk, rtk::Stats* ps)
+{
+    const RtSceneView S = W.S;
+    const int lane = lane_id(), sub = lane & 3, qd = (int)(threadIdx.x >> 2);
+    rtk::QuadStack<RT_QSTACK, 64> stk{s_stk + qd, (float*)s_stk + RT_QSTACK * 64 + qd};
+    const size_t gl = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    rtk::SpillStack<rtk::QuadStack<RT_QSTACK, 64>> xs{stk, W.spill_r + gl * RT_STACK_CAP, W.spill_k + gl * RT_STACK_CAP};
+    const int last_kind = W.any_rays ? rtk::RK_CAM : rtk::RK_BENV;
+    const unsigned long long qlt = (1ull << (lane & ~3)) - 1ull;  // lanes of the quads below
+    bool has_qt = false, act = false;
+    uint32_t qt = 0;  // this quad's QQ ticket
+    uint32_t target = 0;
+    int l = 0;
+    rtk::QState q;
+    for (;;) {
+        // (the counters are loaded before the trip and used after it)
+        uint32_t fin = 0, ab = 0, av = 0;
+        if (lane == 0) {
+            fin = ld_relaxed(A.ctr + A_FIN);
+            ab = ld_relaxed(A.ctr + A_ABORT);
+            av = ld_relaxed(A.ctr + A_QQ_PUSH) - ld_relaxed(A.ctr + A_QQ_TAKE);
+            if (wall_clock64() - t_start > A.limit) {
+                ab = 1;
+                __hip_atomic_store(A.ctr + A_ABORT, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+        bool exact = false, done = false;
+        if (act) {
+            const int res = l ? rtk::quad_visit<true, RT_TAIL_DESCEND>(S, q, stk, sub, ps)
+                              : rtk::quad_visit<false, RT_TAIL_DESCEND>(S, q, stk, sub, ps);
+            if (res != 0) {
+                act = false;
+                float t = 0.0f;
+                int k = 0;
+                const bool ok = res > 0 && (l == 1 || rtk::quad_closest_answer(S, q, sub, t, k, ps));
+                if (ok && sub == 0) {
+                    if (l == 0)
+                        rtk::finish_closest(W, target, q.o, q.d, t, k);
+                    else
+                        rtk::finish_any(W, target, q.h.k == 1);
+                }
+                exact = !ok;
+                done = ok;
+            }
+        }
+        if (exact && sub == 0) {  // the exact octree walk, to completion
+            if (STATS) ps->c[RT_STAT_FALLBACK]++;
+            xs.f = stk;
+            tail_exact(W, l, target, q.o, q.d, xs, ps);
+        }
+        done = done || exact;  // (quad-uniform)
+        bool ready = false;
+        int slot = -1;
+        if (done && sub == 0) {
+            slot = (int)(target >> 3);
+            ready = __hip_atomic_fetch_add(A.pend + slot, -1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == 1;
+        }
+        rq_push(A, n0, ready, slot);
+        // over, or out of time
+        fin = __shfl(fin, 0);
+        if (fin >= n0 || __shfl(ab, 0)) return;
+        const int qq_n = max(0, (int)__shfl(av, 0));
+        // idle quads take what the QQ holds; a quad whose record has arrived starts its walk
+        const bool want = !act && !has_qt;  // (quad-uniform)
+        const unsigned long long bq = __ballot(want && sub == 0);
+        const bool sel = want && __popcll(bq & qlt) < qq_n;
+        const unsigned long long bs = __ballot(sel && sub == 0);
+        if (bs) {
+            const uint32_t t = take_tickets(A.ctr + A_QQ_TAKE, bs, lane & ~3);
+            if (sel) qt = t, has_qt = true;
+        }
+        bool ready2 = false;  // (a query answered without a walk)
+        int slot2 = -1;
+        uint32_t sq = 0;
+        if (!act && has_qt) sq = ld_relaxed(A.qq_seq + (qt & A.qq_mask));
+        sq = (uint32_t)__shfl((int)sq, lane & ~3);  // (one value per quad)
+        if (!act && has_qt) {
+            if (sq == qt + 1u) {
+                // the record past L1 (the sequence word was released after it): lane j of the
+                // quad loads its words 2j, 2j + 1 with an agent-scope load, then the quad shares them
+                const uint64_t* rp = (const uint64_t*)(A.qq + (qt & A.qq_mask));
+                const uint64_t w2 = __hip_atomic_load(rp + sub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const int q0 = lane & ~3;
+                uint32_t wd[8];
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    wd[2 * j] = (uint32_t)__shfl((int)(uint32_t)w2, q0 + j);
+                    wd[2 * j + 1] = (uint32_t)__shfl((int)(uint32_t)(w2 >> 32), q0 + j);
+                }
+                const float4_ ro = float4_{rt_asfloat(wd[0]), rt_asfloat(wd[1]), rt_asfloat(wd[2]), rt_asfloat(wd[3])};
+                const float4_ rd = float4_{rt_asfloat(wd[4]), rt_asfloat(wd[5]), rt_asfloat(wd[6]), rt_asfloat(wd[7])};
+                has_qt = false;
+                target = rt_asuint(rd.w);
+                l = (int)(target & 7u) <= last_kind ? 0 : 1;
+                q.o = rtk::v3of(ro);
+                q.d = rtk::v3of(rd);
+                if (forced_fallback(W, ro, rd)) {
+                    if (sub == 0) {
+                        if (STATS) ps->c[RT_STAT_FALLBACK]++;
+                        xs.f = stk;
+                        tail_exact(W, l, target, q.o, q.d, xs, ps);
+                        slot2 = (int)(target >> 3);
+                        ready2 = __hip_atomic_fetch_add(A.pend + slot2, -1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == 1;
+                    }
+                } else {
+                    act = l ? rtk::qstate_begin<true>(q, q.o, q.d, sub, ps) : rtk::qstate_begin<false>(q, q.o, q.d, sub, ps);
+                    if (!act && sub == 0) {  // (a NaN ray: no hit, answered at once)
+                        if (l == 0)
+                            rtk::finish_closest(W, target, q.o, q.d, -1.0f, -1);
+                        else
+                            rtk::finish_any(W, target, false);
+                        slot2 = (int)(target >> 3);
+                        ready2 = __hip_atomic_fetch_add(A.pend + slot2, -1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == 1;
+                    }
+                }
+            }
+        }
+        rq_push(A, n0, ready2, slot2);
+        if (!__any(act || has_qt)) {  // nothing here: leave once the live paths need fewer walkers
+            if (rank >= max(32, (int)((n0 - fin) / 4u))) return;
+            __builtin_amdgcn_s_sleep(2);
+        }
+    }
+}
+
+template <bool STATS>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TAIL_OCC, RT_TAIL_OCC))) void k_async(rtk::WaveView W, int par, unsigned long long* stats, AsyncQ A)
+{
+    __shared__ uint32_t s_stk[2 * RT_QSTACK * 64];
+    __shared__ int s_pre[RT_QSHARDS + 1];
+    const bool stepper = blockIdx.x % RT_ASYNC_STEP_EVERY == 0;
+    if (stepper) {
+        rtlibm::lds_tables_init();
+        rtk::lds_shade_init(W.S);
+    }
+    const long long t_start = wall_clock64();
+    int32_t* cnt = W.counters;
+    shard_prefix(cnt, RT_QSHARDS, [&](int j) { return ac_at(par, j); }, s_pre);
+    const uint32_t n0 = (uint32_t)s_pre[RT_QSHARDS];
+    // the live list is the RQ's first n0 entries
+    for (int i = (int)(blockIdx.x * blockDim.x + threadIdx.x); i < (int)n0; i += (int)(gridDim.x * blockDim.x)) {
+        const int sh = shard_find(s_pre, RT_QSHARDS, i);
+        const int p = W.act_in[(size_t)sh * W.seg_cap + (i - s_pre[sh])];
+        __hip_atomic_store(A.rq + ((uint32_t)i & A.rq_mask), ((uint64_t)(uint32_t)(i + 1) << 32) | (uint32_t)p,
+                           __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    rtk::Stats st;
+    if (STATS)
+        for (int i = 0; i < RT_STAT_COUNT; i++) st.c[i] = 0;
+    rtk::Stats* ps = STATS ? &st : nullptr;
+    const int bw = (int)(threadIdx.x >> 6), nb = (int)blockDim.x >> 6;
+    if (stepper) {
+        const int rank = (int)(blockIdx.x / RT_ASYNC_STEP_EVERY) * nb + bw;
+        async_stepper<STATS>(W, A, n0, rank, t_start, ps);
+    } else {
+        const int rank = (int)(blockIdx.x - blockIdx.x / RT_ASYNC_STEP_EVERY - 1) * nb + bw;
+        async_walker<STATS>(W, A, n0, rank, t_start, s_stk, ps);
+    }
+    flush_stats<STATS>(st, stats);
+    flush_stats<STATS>(st, stats + RT_STAT_COUNT);  // (the tail kernel's share, for per-kernel byte counts)
+}
+
 __global__ __launch_bounds__(256) void k_intersect(RtSceneView S, const float* __restrict__ rays, int32_t* __restrict__ out,
                                                    int n)
 {
@@ -1231,7 +1556,7 @@ void destroy_one(Backend* b)
     for (DevBuf* d : all)
         if (d->p) (void)hipFree(d->p);
     for (int l = 0; l < RT_MAX_LANES; l++)
-        for (DevBuf* d : {&b->wave[l], &b->counters[l]})
+        for (DevBuf* d : {&b->wave[l], &b->counters[l], &b->aq[l]})
             if (d->p) (void)hipFree(d->p);
     for (int l = 0; l < RT_MAX_LANES; l++) {
         if (b->h_act[l]) (void)hipHostFree(b->h_act[l]);
@@ -1402,6 +1727,7 @@ struct WaveLane {
     long live = 0;  // live paths at the last readback (an upper bound: paths only finish)
     bool done = false, tail_next = false;
     int await = 0;  // 0 none, 1 live count, 2 fallback counts (tail entry check)
+    bool async = false;  // the lane's tail ran as k_async (its abort flag is read back at the end)
     hipEvent_t (*tev)[RT_MAX_TIMED_ITERS] = nullptr;  // [3][RT_MAX_TIMED_ITERS]
 };
 
@@ -1456,7 +1782,15 @@ int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounces, cons
     // 393.5 / 389.6 / 393.1 / - ms (profiles/r03_tail_paths_ab.json)
     double tail_enter = 2.0;
     if (const char* e = getenv("RT_TAIL_ENTER")) tail_enter = atof(e);  // (sweeps)
-    const long tail_max = (long)(tail_enter * tail_blocks * 4 * tail_p / nl);
+    // k_async (RT_ASYNC=1; else k_tail) in place of the tail kernel, entered once a lane's live count
+    // is at most RT_ASYNC_ENTER; RT_ASYNC_LIMIT_S: seconds a launch may run before it gives up
+    int use_async = 0;
+    if (const char* e = getenv("RT_ASYNC")) use_async = atoi(e) != 0;
+    long async_enter = 16384;
+    if (const char* e = getenv("RT_ASYNC_ENTER")) async_enter = std::max(1l, atol(e));
+    double async_limit_s = 60.0;
+    if (const char* e = getenv("RT_ASYNC_LIMIT_S")) async_limit_s = std::max(0.001, atof(e));
+    const long tail_max = use_async ? async_enter : (long)(tail_enter * tail_blocks * 4 * tail_p / nl);
     if (nl > 1) {
         HIPCHK(c, hipEventRecord(b->ev_fork, s));
         for (int l = 1; l < nl; l++) HIPCHK(c, hipStreamWaitEvent(b->ls[l], b->ev_fork, 0));
@@ -1581,6 +1915,40 @@ int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounces, cons
         La.await = 1;
         return RT_OK;
     };
+    // k_async's queues for lane La, sized by its live count at entry (an upper bound), cleared,
+    // then the launch; its abort flag is read back behind it (checked at the end of the render)
+    auto launch_async = [&](WaveLane& La, int par) -> int {
+        const int l = (int)(&La - L);
+        auto pow2 = [](long v) {
+            uint32_t x = 1;
+            while ((long)x < v) x <<= 1;
+            return x;
+        };
+        const uint32_t rq_n = pow2(std::max(4 * La.live, 1l << 20)), qq_n = pow2(std::max(8 * La.live, 1l << 22));
+        const size_t o_rq = 1024, o_qq = o_rq + (size_t)rq_n * 8, o_seq = o_qq + (size_t)qq_n * sizeof(rtk::RayRec);
+        const size_t o_pend = o_seq + (size_t)qq_n * 4, bytes = o_pend + (size_t)La.n * 4;
+        if (int r = ensure(c, b->aq[l], bytes)) return r;
+        char* base = (char*)b->aq[l].p;
+        AsyncQ A;
+        A.ctr = (uint32_t*)base;
+        A.rq = (uint64_t*)(base + o_rq);
+        A.qq = (rtk::RayRec*)(base + o_qq);
+        A.qq_seq = (uint32_t*)(base + o_seq);
+        A.pend = (int32_t*)(base + o_pend);
+        A.rq_mask = rq_n - 1;
+        A.qq_mask = qq_n - 1;
+        A.limit = (long long)(async_limit_s * 1e8);
+        HIPCHK(c, hipMemsetAsync(base, 0, o_qq, La.s));  // counters and the RQ's sequence words
+        HIPCHK(c, hipMemsetAsync(A.qq_seq, 0, (size_t)qq_n * 4, La.s));
+        if (S)
+            hipLaunchKernelGGL(k_async<true>, dim3(tail_blocks), dim3(threads), 0, La.s, La.W, par, stats, A);
+        else
+            hipLaunchKernelGGL(k_async<false>, dim3(tail_blocks), dim3(threads), 0, La.s, La.W, par, stats, A);
+        HIPCHK(c, hipGetLastError());
+        HIPCHK(c, hipMemcpyAsync(La.h + act_bytes / 4 + 8, A.ctr + A_ABORT, 4, hipMemcpyDeviceToHost, La.s));
+        La.async = true;
+        return RT_OK;
+    };
     // enqueue up to 8 iterations, then a readback
     auto issue = [&](WaveLane& La) -> int {
         for (int k = 0; k < 8 && La.it < max_iters; k++) {
@@ -1606,11 +1974,15 @@ int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounces, cons
             if (f[C_FBC0 + par] == 0 && f[C_FBA0 + par] == 0 && f[C_PARKC0 + (par ^ 1)] == 0 &&
                 f[C_PARKA0 + (par ^ 1)] == 0) {  // (k_trace(i) released DONE[par ^ 1])
                 // few paths left and none waits: the tail kernel finishes them all
-                HIPCHK(c, hipMemsetAsync(La.cnt + C_TK_TAIL, 0, 4, La.s));
-                if (S)
-                    hipLaunchKernelGGL(k_tail<true>, dim3(tail_blocks), dim3(threads), 0, La.s, La.W, par, stats);
-                else
-                    hipLaunchKernelGGL(k_tail<false>, dim3(tail_blocks), dim3(threads), 0, La.s, La.W, par, stats);
+                if (use_async) {
+                    if (int r = launch_async(La, par)) return r;
+                } else {
+                    HIPCHK(c, hipMemsetAsync(La.cnt + C_TK_TAIL, 0, 4, La.s));
+                    if (S)
+                        hipLaunchKernelGGL(k_tail<true>, dim3(tail_blocks), dim3(threads), 0, La.s, La.W, par, stats);
+                    else
+                        hipLaunchKernelGGL(k_tail<false>, dim3(tail_blocks), dim3(threads), 0, La.s, La.W, par, stats);
+                }
                 if (b->timing && La.it < RT_MAX_TIMED_ITERS) HIPCHK(c, hipEventRecord(La.tev[2][La.it], La.s));
                 HIPCHK(c, hipGetLastError());
                 La.tail_iter = La.it;
@@ -1664,6 +2036,15 @@ int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounces, cons
     b->tail_iter = L[0].tail_iter;
     HIPCHK(c, hipEventRecord(b->ev_done, s));
     b->done_recorded = true;
+    bool any_async = false;
+    for (int l = 0; l < nl; l++) any_async = any_async || L[l].async;
+    if (any_async) {  // a k_async launch that ran out of time left paths unfinished: fail loudly
+        HIPCHK(c, hipStreamSynchronize(s));
+        for (int l = 0; l < nl; l++)
+            if (L[l].async && L[l].h[act_bytes / 4 + 8] != 0)
+                return rt_fail(c, RT_ERR_STATE, "render: the async tail kernel (k_async) did not finish in " +
+                                                    std::to_string(async_limit_s) + " s (RT_ASYNC_LIMIT_S)");
+    }
     if (S && iter_log) {
         std::vector<int32_t> hq((size_t)6 * RT_MAX_TIMED_ITERS);
         HIPCHK(c, hipMemcpyAsync(hq.data(), b->iterq.p, hq.size() * 4, hipMemcpyDeviceToHost, s));
