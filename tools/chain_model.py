@@ -57,6 +57,7 @@ def main():
     ap.add_argument("--floor-us", type=float, default=150.0)
     ap.add_argument("--tail-n", type=float, default=8192)
     ap.add_argument("--tail-us", type=float, default=74.0)
+    ap.add_argument("--out", default="")
     args = ap.parse_args()
     z = np.load(args.log)
     d = z["draws"].astype(np.int32)
@@ -74,10 +75,10 @@ def main():
     t_ideal = args.t1_ms / world
     out = []
     pols = [("base K=1", 1, 1, 0, 1, 0)]
-    for t_spec in (0, 150, 220, 260, 300):
-        for k in (2, 4, 8, 16):
-            pols.append((f"K={k} from it {t_spec}", 1, k, t_spec, 1, 0))
-            pols.append((f"K={k} from it {t_spec} last-b", 1, k, t_spec, 1, 1))
+    for t_spec in (0, 260, 300):
+        for k in (2, 4, 8):
+            pols.append((f"window K={k} from it {t_spec}, b=1", 1, k, t_spec, 1, 0))
+            pols.append((f"window K={k} from it {t_spec}, last b", 1, k, t_spec, 1, 1))
     for name, klo, khi, ts, pr, pm in pols:
         hist, fin, work = run(L, b, klo, khi, ts, pr, pm)
         ms = frame_ms(hist, scale, unit_ns, args.floor_us, args.tail_n, args.tail_us)
@@ -85,6 +86,34 @@ def main():
              "eff": round(t_ideal / ms, 3)}
         out.append(r)
         print(json.dumps(r), flush=True)
+    L.lattice_sim.restype = ctypes.c_long
+    L.lattice_sim.argtypes = [ctypes.c_void_p] + [ctypes.c_int] * 5 + [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
+                                                                       ctypes.c_void_p]
+    for t0 in (266, 500, 873):
+        for R in (4, 8, 16, 32):
+            hist = np.zeros(20000, np.int32)
+            fin = np.zeros(b.shape[0], np.int32)
+            work = np.zeros(1, np.int64)
+            tm = L.lattice_sim(b.ctypes.data, b.shape[0], b.shape[1], R, t0, 8, hist.ctypes.data, 20000,
+                               fin.ctypes.data, work.ctypes.data)
+            hist = hist[:tm + 1]
+            ms = frame_ms(hist, scale, unit_ns, args.floor_us, args.tail_n, args.tail_us)
+            r = {"policy": f"lattice R={R} from it {t0}", "iters": int(tm), "work_x": round(int(work[0]) / chain.sum(), 3),
+                 "ms": round(ms, 1), "eff": round(t_ideal / ms, 3)}
+            out.append(r)
+            print(json.dumps(r), flush=True)
+    if args.out:
+        summary = {"what": "per-pixel sample-chain model of an N-way row shard (tools/chain_model.py on tools/chain_log.py's "
+                           "per-sample draw counts from the CPU restatement; analysis only)",
+                   "log": {"config": str(z.get("config", "cfg4")), "world": world, "rank": int(z["rank"]), "every": every,
+                           "pixels": int(b.shape[0])},
+                   "chains": {"mean": float(chain.mean()), "p99": float(np.percentile(chain, 99)), "max": int(chain.max()),
+                              "b_hist": np.bincount(b.ravel()).tolist()},
+                   "time_model": {"unit_ns_per_path_step": round(unit_ns, 4), "floor_us": args.floor_us,
+                                  "tail_below_paths": args.tail_n, "tail_round_us": args.tail_us, "t1_ms": args.t1_ms},
+                   "policies": out}
+        with open(args.out, "w") as f:
+            json.dump(summary, f, indent=1)
 
 
 if __name__ == "__main__":
