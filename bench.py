@@ -542,7 +542,7 @@ def main():
         torch.cuda.synchronize(dev)
         lane1_ms = (time.perf_counter() - t1) * 1e3
         ktime = rk.kernel_timing(0)
-        rk.set_lanes(3)
+        rk.set_lanes(0)  # (auto)
         log(f"[rank {rank}] 1-lane render {lane1_ms:.1f} ms, kernel time per class {ktime}")
 
     samples_rank = frame.rows * W * spp if not single_process_multi else W * H * spp

@@ -47,6 +47,7 @@ namespace {
 
 #define RT_MAX_TIMED_ITERS 16384
 #define RT_MAX_LANES 4  // wavefront lanes (streams) per render (run_wave)
+#define RT_LANES4_MAX 1572864  // auto lanes: 4 at most this many slots per launch, else 3
 #ifndef RT_STEP_OCC
 #define RT_STEP_OCC 3  // k_step waves per SIMD
 #endif
@@ -164,7 +165,10 @@ struct Backend {
     bool done_recorded = false;
     hipStream_t ls[RT_MAX_LANES] = {};      // lanes 1.. streams (lane 0 runs on the caller's)
     hipEvent_t ev_fork = nullptr, ev_join[RT_MAX_LANES] = {}, ev_lane[RT_MAX_LANES] = {};
-    int lanes = 3;                          // RT_LANES (sweep on cfg2: 452 / 499 / 519 / 509 Msamples/s for 1-4)
+    int lanes = 0;                          // RT_LANES; 0: auto, 4 lanes for launches of at most RT_LANES4_MAX
+                                            // slots, else 3 (cfg2 1-4 lanes: 452 / 499 / 519 / 509 Msamples/s, r01;
+                                            // r03: 3 / 4 lanes cfg2 147.5 / 148.6 ms, cfg4 8-way shard 398 / 386 ms,
+                                            // 6 / 8 lanes 230-710 ms: more streams than the 4 hardware queues)
     RtSceneView view{};
     int bl_rays = 1, any_rays = 1;
     int last_iters = 0;
@@ -1824,7 +1828,7 @@ int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounces, cons
         HIPCHK(c, hipMemsetAsync(b->iterq.p, 0, RT_MAX_TIMED_ITERS * 24, s));
     }
     // lanes: rows interleave (row j of the launch -> lane j % lanes); pixel lists split in runs
-    int nl = b->lanes;
+    int nl = b->lanes > 0 ? b->lanes : n <= RT_LANES4_MAX ? 4 : 3;
     const int rows = src.xy ? 0 : n / src.W;
     while (nl > 1 && (n < nl * 65536 || (!src.xy && rows < nl))) nl--;
     WaveLane L[RT_MAX_LANES];
@@ -2607,10 +2611,10 @@ extern "C" int rt_device_kernel_timing(rt_context* c, int enable, double* out_ms
 }
 
 // Wavefront lanes (streams) per render on every device of the context (RT_LANES at
-// creation; 1 serializes a render's launches, for per-launch kernel timing).
+// creation; 1 serializes a render's launches, for per-launch kernel timing; 0: auto).
 extern "C" int rt_device_set_lanes(rt_context* c, int lanes)
 {
-    if (!c || !c->backend || lanes < 1) return RT_ERR_ARG;
+    if (!c || !c->backend || lanes < 0) return RT_ERR_ARG;
     for (Backend* b : grp(c)->dev) b->lanes = std::min(RT_MAX_LANES, lanes);
     return RT_OK;
 }

@@ -348,7 +348,8 @@ class RenderKernel:
         return {k: (float(a), int(b)) for k, a, b in zip(("trace", "step", "other"), ms, n)}
 
     def set_lanes(self, lanes: int):
-        """Wavefront lanes (streams) per render on every device (1: launches serialized)."""
+        """Wavefront lanes (streams) per render on every device (1: launches serialized; 0: auto,
+        4 for launches of at most 1.5 M pixels, else 3)."""
         check(self.L, self.L.rt_device_set_lanes(self.ctx, int(lanes)), self.ctx, "rt_device_set_lanes")
 
     def last_iterations(self) -> int:

@@ -4,7 +4,8 @@ settings, in one process (run_wave reads its knobs at every render).
   python tools/knob_probe.py --sets "RT_TAIL_PATHS=2,RT_TAIL_ENTER=2" "RT_TAIL_PATHS=8,RT_TAIL_ENTER=2" \
       [--world 8 --rank 1] [--reps 3] [--rounds 2] [--out gpurun_out/knob_probe.json]
 
-Settings alternate round by round (A B C A B C ...), min over reps per round.
+Settings alternate round by round (A B C A B C ...), min over reps per round. LANES=k sets the
+context's wavefront lanes (rt_device_set_lanes; default 0 = auto).
 """
 from __future__ import annotations
 
@@ -50,10 +51,15 @@ def main():
         for k in list(os.environ):
             if k.startswith("RT_") and k not in base_env:
                 del os.environ[k]
+        lanes = 0  # (auto)
         if s != "-":
             for kv in s.split(","):
                 k, v = kv.split("=", 1)
-                os.environ[k] = v
+                if k == "LANES":  # (wavefront lanes of the context: rt_device_set_lanes)
+                    lanes = int(v)
+                else:
+                    os.environ[k] = v
+        rk.set_lanes(lanes)
 
     def timed(cfg):
         if cfg == "cfg4":
