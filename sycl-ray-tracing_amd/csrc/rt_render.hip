@@ -1849,7 +1849,10 @@ int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounces, cons
     // list): with 2 paths per wave, RT_TAIL_ENTER = 1.4 / 1.75 / 2.2 / 2.8 -> cfg2 888-897 /
     // 891-898 / 893-897 / 874-879 Msamples/s (5 paths at 0.7: 888-892), cfg4 8-way shard
     // 393.5 / 389.6 / 393.1 / - ms (profiles/r03_tail_paths_ab.json)
-    double tail_enter = 2.0;
+    // (4 lanes, the auto count of launches of <= 1.5 M slots: 1.4 — cfg4 8-way shard, 4 rounds on
+    // one MI355X: 2.0 / 1.5 / 1.25 / 1.0 -> 384-391 / 380-384 / 379-383 / 382-390 ms,
+    // profiles/r03_tail_enter4.json)
+    double tail_enter = nl == 4 ? 1.4 : 2.0;
     if (const char* e = getenv("RT_TAIL_ENTER")) tail_enter = atof(e);  // (sweeps)
     // k_async (RT_ASYNC=1; else k_tail) in place of the tail kernel (RT_TAIL_PATHS=0: neither), entered
     // once a lane's live count is at most RT_ASYNC_ENTER; RT_ASYNC_LIMIT_S: seconds a launch may run
