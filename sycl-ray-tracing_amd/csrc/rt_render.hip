@@ -155,8 +155,6 @@ struct Backend {
     DevBuf iterq;     // stats renders: per-iteration {queries, live slots} (RT_ITER_LOG)
     DevBuf wave[RT_MAX_LANES];      // per lane: path state, pending records, results, queues, lists
     DevBuf counters[RT_MAX_LANES];  // per lane: C_COUNT int32
-    DevBuf aq[RT_MAX_LANES];        // per lane: k_async's queues (AsyncQ)
-    DevBuf aprof;                   // RT_ASYNC_PROF counters
     DevBuf xy;        // pixel list (rt_render_pixels)
     DevBuf fb;        // host-fb staging
     int32_t* h_act[RT_MAX_LANES] = {};     // per lane, pinned: live-slot counters (sharded) + 8 fallback counters
@@ -1019,394 +1017,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TAIL_OCC
     flush_stats<STATS>(st, stats + RT_STAT_COUNT);  // (the tail kernel's share, for per-kernel byte counts)
 }
 
-// ------------------------------------------------------------- async kernel
-// k_async: the tail kernel without a path's wave. Once the live count is low, an iteration
-// of the wavefront costs its slowest walk plus a step launch however few paths it carries,
-// and k_tail's waves own their paths, so a path's round waits for the walks of the other
-// paths of its wave. Here paths and queries move through queues:
-//   RQ  ready paths (every query of the last step answered): a stepper lane takes one and
-//       steps it; the step's rays go to the QQ with the path's pend count set to their
-//       number (a path with no rays goes straight back to the RQ, a finished one is counted);
-//   QQ  queries: an idle quad of a walker wave takes one and walks it (rt_quad.h quad_visit,
-//       the exact octree walk inline when the quad walk cannot settle it); the walk that
-//       answers a path's last query puts the path back in the RQ.
-// No wave ever blocks on another: a queue entry is taken by ticket (its position), and a
-// lane or quad whose entry is not written yet checks again on its next loop.
-//
-// XCD-local: per-XCD L2s are not coherent with each other, and a release / acquire pair at
-// agent scope writes back / invalidates caches (MI355X_MICROARCH.md, inter-workgroup
-// visibility: ~1.7-6.5 us each; with them on every hand-off, a first version of this
-// kernel ran cfg2 at 180 ms against k_tail's 146). So path p belongs to XCD p % 8, every
-// queue is per XCD, and a block serves the XCD it runs on (HW_REG_XCC_ID): a hand-off
-// never leaves the XCD's L2. Producer: plain stores (L1 is write-through) -> s_waitcnt
-// vmcnt(0) -> the sequence word; consumer: polls with agent-scope (L1-bypassing) loads,
-// and a stepper invalidates its L1 (agent acquire) before path_step's plain loads. The
-// pend counts live beyond L2 (agent atomics), so the step's pend store is an atomic too.
-// A path's step happens once all of its queries are answered, exactly as in the wavefront,
-// so the answers are bit-identical.
-struct AsyncQ {
-    uint32_t* ctr;      // counters (A_*), one 128-B line each
-    uint64_t* rq;       // 8 rings (one per XCD) of rq_mask + 1 entries: (position + 1) << 32 | slot
-    rtk::RayRec* qq;    // 8 rings of qq_mask + 1 queue records (o.w = slot bits, d.w = target bits)
-    uint32_t* qq_seq;   // position + 1 once the record at that position is written
-    int32_t* pend;      // [n_slots] queries of the path's last step not answered yet
-    uint32_t rq_mask, qq_mask;
-    long long limit;    // wall_clock64 ticks (100 MHz) a wave may run before the launch gives up
-    unsigned long long* prof;  // RT_ASYNC_PROF: per-launch counters (AP_*), else null
-    int step_every;     // of an XCD's blocks, every step_every-th steps paths, the others walk queries
-    int calls;          // walker: quad_visit calls per loop before its bookkeeping
-    int refill;         // walker: idle quads that take new queries together
-};
-#define A_FIN 0
-#define A_ABORT 32
-#define A_XCD 64                // per XCD x at A_XCD + 256 x: RQ take, RQ push, QQ take, QQ push, blocks, live-list scan
-#define A_COUNT (A_XCD + 8 * 256)
-__device__ __forceinline__ uint32_t* actr(const AsyncQ& A, int x, int k) { return A.ctr + A_XCD + 256 * x + 32 * k; }
-enum { AX_RQ_TAKE, AX_RQ_PUSH, AX_QQ_TAKE, AX_QQ_PUSH, AX_BLOCKS, AX_SCAN };
-enum { AP_SLOOPS, AP_SIDLE, AP_STEPS, AP_PATHS, AP_STEP_TICKS, AP_WLOOPS, AP_WIDLE, AP_VISITS, AP_TAKEN, AP_WAVES_S,
-       AP_WAVES_W, AP_S_TICKS, AP_W_TICKS, AP_COUNT };
-
-__device__ __forceinline__ uint32_t ld_relaxed(const uint32_t* p)
-{
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void vm_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
-__device__ __forceinline__ int xcc_id()
-{
-    int v;
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(v));
-    return v & 7;
-}
-
-// Wave-aggregated ticket: the lanes of b get consecutive positions of the counter; lane_bit
-// is the bit of b that stands for the calling lane (its quad's first lane for quads).
-__device__ __forceinline__ uint32_t take_tickets(uint32_t* ctr, unsigned long long b, int lane_bit)
-{
-    const int leader = __ffsll((long long)b) - 1;
-    uint32_t base = 0;
-    if (lane_id() == leader) base = atomicAdd(ctr, (uint32_t)__popcll(b));
-    base = __shfl(base, leader);
-    return base + (uint32_t)__popcll(b & ((1ull << lane_bit) - 1ull));
-}
-
-// The lanes with `want` put `slot` in XCD x's RQ (converged call; the caller has drained
-// the stores the path's step will read).
-__device__ __forceinline__ void rq_push(const AsyncQ& A, int x, bool want, int slot)
-{
-    const unsigned long long b = __ballot(want);
-    if (!b) return;
-    const uint32_t pos = take_tickets(actr(A, x, AX_RQ_PUSH), b, lane_id());
-    if (want) A.rq[(size_t)x * (A.rq_mask + 1) + (pos & A.rq_mask)] = ((uint64_t)(pos + 1u) << 32) | (uint32_t)slot;
-}
-
-// Steps the paths the lanes hold (my >= 0), out of line like tail_step: the step's rays to
-// XCD x's QQ (pend = their number first), a path without rays back to the RQ, a finished
-// path counted. Converged call.
-__device__ __noinline__ void async_step(const rtk::WaveView& W, const AsyncQ& A, int my, int x, rtk::Stats* ps)
-{
-    rtk::Emit e;
-    e.mask = 0;
-    e.active = false;
-    e.heavy = false;
-    if (my >= 0) rtk::path_step(W, my, e, ps);
-    const int nr = __popc(e.mask);
-    if (my >= 0 && nr > 0) __hip_atomic_store(A.pend + my, nr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    unsigned long long b[rtk::RK_COUNT];
-    int tot = 0;
-#pragma unroll
-    for (int k = 0; k < rtk::RK_COUNT; k++) {
-        b[k] = __ballot((e.mask >> k) & 1u);
-        tot += __popcll(b[k]);
-    }
-    uint32_t base = 0;
-    if (tot > 0) {
-        if (lane_id() == 0) base = atomicAdd(actr(A, x, AX_QQ_PUSH), (uint32_t)tot);
-        base = __shfl(base, 0);
-    }
-    const unsigned long long lt = (1ull << lane_id()) - 1ull;
-    rtk::RayRec* qq = A.qq + (size_t)x * (A.qq_mask + 1);
-    uint32_t* seq = A.qq_seq + (size_t)x * (A.qq_mask + 1);
-    uint32_t pos[rtk::RK_COUNT];
-    {
-        uint32_t bb = base;
-#pragma unroll
-        for (int k = 0; k < rtk::RK_COUNT; k++) {
-            pos[k] = bb + (uint32_t)__popcll(b[k] & lt);
-            if ((e.mask >> k) & 1u) qq[pos[k] & A.qq_mask] = e.rec(k, my, rt_asfloat(((uint32_t)my << 3) | (uint32_t)k));
-            bb += (uint32_t)__popcll(b[k]);
-        }
-    }
-    vm_drain();  // the path's state, its pend word and the records, before any sequence word
-#pragma unroll
-    for (int k = 0; k < rtk::RK_COUNT; k++)
-        if ((e.mask >> k) & 1u) seq[pos[k] & A.qq_mask] = pos[k] + 1u;
-    rq_push(A, x, my >= 0 && e.active && nr == 0, my);
-    const unsigned long long bf = __ballot(my >= 0 && !e.active);
-    if (bf && lane_id() == 0) atomicAdd(A.ctr + A_FIN, (uint32_t)__popcll(bf));
-}
-
-// Over (every path finished) or out of time (a safety net: the host reports RT_ERR_STATE).
-__device__ __forceinline__ bool async_over(const AsyncQ& A, uint32_t n0, long long t_start, uint32_t& fin)
-{
-    uint32_t f = 0, ab = 0;
-    if (lane_id() == 0) {
-        f = ld_relaxed(A.ctr + A_FIN);
-        ab = ld_relaxed(A.ctr + A_ABORT);
-        if (wall_clock64() - t_start > A.limit) {
-            ab = 1;
-            __hip_atomic_store(A.ctr + A_ABORT, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
-    fin = __shfl(f, 0);
-    return fin >= n0 || __shfl(ab, 0);
-}
-
-template <int N>
-__device__ __forceinline__ void prof_flush(const AsyncQ& A, unsigned long long (&pr)[N])
-{
-    if (A.prof && lane_id() == 0)
-        for (int i = 0; i < N; i++)
-            if (pr[i]) atomicAdd(A.prof + i, pr[i]);
-}
-
-// A stepper wave of XCD x: its lanes take ready paths, step those that have arrived.
-__device__ __forceinline__ void async_stepper(const rtk::WaveView& W, const AsyncQ& A, uint32_t n0, int x, int rank,
-                                              long long t_start, rtk::Stats* ps)
-{
-    const int lane = lane_id();
-    const unsigned long long lt = (1ull << lane) - 1ull;
-    const uint64_t* rq = A.rq + (size_t)x * (A.rq_mask + 1);
-    bool has_rt = false;
-    uint32_t rt = 0;  // this lane's RQ ticket
-    uint32_t fin = 0;
-    unsigned long long pr[AP_COUNT] = {};
-    const long long t0 = wall_clock64();
-    for (;;) {
-        pr[AP_SLOOPS]++;
-        if (async_over(A, n0, t_start, fin)) break;
-        uint32_t av = 0;
-        if (lane == 0) av = ld_relaxed(actr(A, x, AX_RQ_PUSH)) - ld_relaxed(actr(A, x, AX_RQ_TAKE));
-        const int rq_n = max(0, (int)__shfl(av, 0));
-        if (!__any(has_rt) && rq_n == 0) {  // nothing here: leave once the live paths need fewer steppers
-            pr[AP_SIDLE]++;
-            if (rank >= max(1, (int)((n0 - fin) / 256u))) break;
-            __builtin_amdgcn_s_sleep(2);
-            continue;
-        }
-        const unsigned long long bw = __ballot(!has_rt);
-        const bool sel = !has_rt && __popcll(bw & lt) < rq_n;
-        const unsigned long long bs = __ballot(sel);
-        if (bs) {
-            const uint32_t t = take_tickets(actr(A, x, AX_RQ_TAKE), bs, lane);
-            if (sel) rt = t, has_rt = true;
-        }
-        int my = -1;
-        if (has_rt) {
-            const uint64_t v = __hip_atomic_load(rq + (rt & A.rq_mask), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if ((uint32_t)(v >> 32) == rt + 1u) {
-                my = (int)(uint32_t)v;
-                has_rt = false;
-            }
-        }
-        if (__any(my >= 0)) {
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // (this CU's L1: the path's state and answers)
-            const long long ts = wall_clock64();
-            async_step(W, A, my, x, ps);
-            pr[AP_STEPS]++;
-            pr[AP_PATHS] += (unsigned long long)__popcll(__ballot(my >= 0));
-            pr[AP_STEP_TICKS] += (unsigned long long)(wall_clock64() - ts);
-        }
-    }
-    pr[AP_WAVES_S] = 1;
-    pr[AP_S_TICKS] = (unsigned long long)(wall_clock64() - t0);
-    prof_flush(A, pr);
-}
-
-// A walker wave of XCD x: each quad walks one query at a time, one trip per loop; idle
-// quads take queries; the walk that answers a path's last query puts the path in the RQ.
-template <bool STATS>
-__device__ __forceinline__ void async_walker(const rtk::WaveView& W, const AsyncQ& A, uint32_t n0, int x, int rank,
-                                             long long t_start, uint32_t* s_stk, rtk::Stats* ps)
-{
-    const RtSceneView S = W.S;
-    const int lane = lane_id(), sub = lane & 3, qd = (int)(threadIdx.x >> 2);
-    rtk::QuadStack<RT_QSTACK, 64> stk{s_stk + qd, (float*)s_stk + RT_QSTACK * 64 + qd};
-    const size_t gl = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    rtk::SpillStack<rtk::QuadStack<RT_QSTACK, 64>> xs{stk, W.spill_r + gl * RT_STACK_CAP, W.spill_k + gl * RT_STACK_CAP};
-    const int last_kind = W.any_rays ? rtk::RK_CAM : rtk::RK_BENV;
-    const unsigned long long qlt = (1ull << (lane & ~3)) - 1ull;  // lanes of the quads below
-    const rtk::RayRec* qq = A.qq + (size_t)x * (A.qq_mask + 1);
-    const uint32_t* seq = A.qq_seq + (size_t)x * (A.qq_mask + 1);
-    bool has_qt = false, act = false;
-    uint32_t qt = 0;  // this quad's QQ ticket
-    uint32_t target = 0;
-    int l = 0, loops = 0;
-    uint32_t fin = 0;
-    rtk::QState q;
-    unsigned long long pr[AP_COUNT] = {};
-    const long long t0 = wall_clock64();
-    for (;; loops++) {
-        pr[AP_WLOOPS]++;
-        pr[AP_VISITS] += (unsigned long long)__popcll(__ballot(act && sub == 0));
-        // (the counters are loaded before the trip and used after it)
-        uint32_t av = 0;
-        if (lane == 0) av = ld_relaxed(actr(A, x, AX_QQ_PUSH)) - ld_relaxed(actr(A, x, AX_QQ_TAKE));
-        bool done = false;  // (quad-uniform) this quad answered its query in this loop
-        for (int c = 0; c < A.calls && __any(act); c++) {  // a few trips before the bookkeeping
-            bool exact = false;
-            if (act) {
-                const int res = l ? rtk::quad_visit<true, RT_TAIL_DESCEND>(S, q, stk, sub, ps)
-                                  : rtk::quad_visit<false, RT_TAIL_DESCEND>(S, q, stk, sub, ps);
-                if (res != 0) {
-                    act = false;
-                    float t = 0.0f;
-                    int k = 0;
-                    const bool ok = res > 0 && (l == 1 || rtk::quad_closest_answer(S, q, sub, t, k, ps));
-                    if (ok && sub == 0) {
-                        if (l == 0)
-                            rtk::finish_closest(W, target, q.o, q.d, t, k);
-                        else
-                            rtk::finish_any(W, target, q.h.k == 1);
-                    }
-                    exact = !ok;
-                    done = true;
-                }
-            }
-            if (exact && sub == 0) {  // the exact octree walk, to completion
-                if (STATS) ps->c[RT_STAT_FALLBACK]++;
-                xs.f = stk;
-                tail_exact(W, l, target, q.o, q.d, xs, ps);
-            }
-        }
-        const int qq_n = max(0, (int)__shfl(av, 0));
-        // idle quads take what the QQ holds, once enough of them are idle (or none walks)
-        const bool want = !act && !has_qt && !done;  // (quad-uniform)
-        const unsigned long long bq0 = __ballot(want && sub == 0);
-        const unsigned long long bq = (__popcll(bq0) >= A.refill || !__any(act)) ? bq0 : 0ull;
-        const bool sel = want && bq != 0ull && __popcll(bq & qlt) < qq_n;
-        const unsigned long long bs = __ballot(sel && sub == 0);
-        if (bs) {
-            const uint32_t t = take_tickets(actr(A, x, AX_QQ_TAKE), bs, lane & ~3);
-            if (sel) qt = t, has_qt = true;
-            pr[AP_TAKEN] += (unsigned long long)__popcll(bs);
-        }
-        // a quad whose record has arrived starts its walk
-        uint32_t sq = 0;
-        if (!act && has_qt) sq = ld_relaxed(seq + (qt & A.qq_mask));
-        sq = (uint32_t)__shfl((int)sq, lane & ~3);  // (one value per quad)
-        if (!act && has_qt && sq == qt + 1u) {
-            // the record (L1-bypassing loads, served by the XCD's L2): lane j of the quad loads
-            // its words 2j, 2j + 1, then the quad shares them
-            const uint64_t* rp = (const uint64_t*)(qq + (qt & A.qq_mask));
-            const uint64_t w2 = __hip_atomic_load(rp + sub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const int q0 = lane & ~3;
-            uint32_t wd[8];
-#pragma unroll
-            for (int j = 0; j < 4; j++) {
-                wd[2 * j] = (uint32_t)__shfl((int)(uint32_t)w2, q0 + j);
-                wd[2 * j + 1] = (uint32_t)__shfl((int)(uint32_t)(w2 >> 32), q0 + j);
-            }
-            const float4_ ro = float4_{rt_asfloat(wd[0]), rt_asfloat(wd[1]), rt_asfloat(wd[2]), rt_asfloat(wd[3])};
-            const float4_ rd = float4_{rt_asfloat(wd[4]), rt_asfloat(wd[5]), rt_asfloat(wd[6]), rt_asfloat(wd[7])};
-            has_qt = false;
-            target = rt_asuint(rd.w);
-            l = (int)(target & 7u) <= last_kind ? 0 : 1;
-            q.o = rtk::v3of(ro);
-            q.d = rtk::v3of(rd);
-            if (forced_fallback(W, ro, rd)) {
-                if (sub == 0) {
-                    if (STATS) ps->c[RT_STAT_FALLBACK]++;
-                    xs.f = stk;
-                    tail_exact(W, l, target, q.o, q.d, xs, ps);
-                }
-                done = true;
-            } else {
-                act = l ? rtk::qstate_begin<true>(q, q.o, q.d, sub, ps) : rtk::qstate_begin<false>(q, q.o, q.d, sub, ps);
-                if (!act) {  // (a NaN ray: no hit, answered at once)
-                    if (sub == 0) {
-                        if (l == 0)
-                            rtk::finish_closest(W, target, q.o, q.d, -1.0f, -1);
-                        else
-                            rtk::finish_any(W, target, false);
-                    }
-                    done = true;
-                }
-            }
-        }
-        // answered queries: the answer drained, then the path's pend count; the last one
-        // sends the path back to the RQ
-        bool ready = false;
-        int slot = -1;
-        if (__any(done)) {
-            vm_drain();
-            if (done && sub == 0) {
-                slot = (int)(target >> 3);
-                ready = __hip_atomic_fetch_add(A.pend + slot, -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 1;
-            }
-            rq_push(A, x, ready, slot);
-        }
-        if (!__any(act || has_qt)) {  // nothing here: leave once the live paths need fewer walkers
-            pr[AP_WIDLE]++;
-            if (async_over(A, n0, t_start, fin)) break;
-            if (rank >= max(1, (int)((n0 - fin) / 32u))) break;
-            __builtin_amdgcn_s_sleep(2);
-        } else if ((loops & 15) == 0) {
-            if (async_over(A, n0, t_start, fin)) break;
-        }
-    }
-    pr[AP_WAVES_W] = 1;
-    pr[AP_W_TICKS] = (unsigned long long)(wall_clock64() - t0);
-    prof_flush(A, pr);
-}
-
-template <bool STATS>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TAIL_OCC, RT_TAIL_OCC))) void k_async(rtk::WaveView W, int par, unsigned long long* stats, AsyncQ A)
-{
-    __shared__ uint32_t s_stk[2 * RT_QSTACK * 64];
-    __shared__ int s_pre[RT_QSHARDS + 1];
-    __shared__ int s_role;
-    const long long t_start = wall_clock64();
-    const int x = xcc_id();
-    if (threadIdx.x == 0) s_role = (int)atomicAdd(actr(A, x, AX_BLOCKS), 1u);  // this block's number on its XCD
-    int32_t* cnt = W.counters;
-    shard_prefix(cnt, RT_QSHARDS, [&](int j) { return ac_at(par, j); }, s_pre);  // (syncs: s_role is set)
-    const int bix = s_role;
-    const bool stepper = bix % A.step_every == 0;
-    if (stepper) {
-        rtlibm::lds_tables_init();
-        rtk::lds_shade_init(W.S);
-    }
-    const uint32_t n0 = (uint32_t)s_pre[RT_QSHARDS];
-    // the live list into the RQs, path p to XCD p % 8: the blocks of each XCD scan the whole
-    // list in 64-entry chunks (a per-XCD cursor) and enqueue their XCD's paths, so even these
-    // entries are written and read within one L2
-    for (;;) {
-        uint32_t c0 = 0;
-        if (lane_id() == 0) c0 = atomicAdd(actr(A, x, AX_SCAN), 64u);
-        c0 = __shfl(c0, 0);
-        if (c0 >= n0) break;
-        const int i = (int)c0 + lane_id();
-        int p = -1;
-        if (i < (int)n0) {
-            const int sh = shard_find(s_pre, RT_QSHARDS, i);
-            p = W.act_in[(size_t)sh * W.seg_cap + (i - s_pre[sh])];
-        }
-        const bool mine = p >= 0 && (p & 7) == x;
-        rq_push(A, x, mine, p);
-    }
-    rtk::Stats st;
-    if (STATS)
-        for (int i = 0; i < RT_STAT_COUNT; i++) st.c[i] = 0;
-    rtk::Stats* ps = STATS ? &st : nullptr;
-    const int wv = (int)(threadIdx.x >> 6), nb = (int)blockDim.x >> 6;
-    if (stepper)
-        async_stepper(W, A, n0, x, (bix / A.step_every) * nb + wv, t_start, ps);
-    else
-        async_walker<STATS>(W, A, n0, x, (bix - bix / A.step_every - 1) * nb + wv, t_start, s_stk, ps);
-    flush_stats<STATS>(st, stats);
-    flush_stats<STATS>(st, stats + RT_STAT_COUNT);  // (the tail kernel's share, for per-kernel byte counts)
-}
-
 __global__ __launch_bounds__(256) void k_intersect(RtSceneView S, const float* __restrict__ rays, int32_t* __restrict__ out,
                                                    int n)
 {
@@ -1621,11 +1231,11 @@ void destroy_one(Backend* b)
     (void)hipDeviceSynchronize();
     DevBuf* all[] = {&b->nodes, &b->tri4, &b->prim2k, &b->mat_idx, &b->mats, &b->emissive, &b->spheres, &b->env,
                      &b->env_lum, &b->cdf, &b->bvh4, &b->bvh_tri4, &b->parent, &b->leaf_of, &b->cdf_row, &b->cdf_coarse,
-                     &b->cdf_fence, &b->matk, &b->stats, &b->xy, &b->fb, &b->iterq, &b->aprof};
+                     &b->cdf_fence, &b->matk, &b->stats, &b->xy, &b->fb, &b->iterq};
     for (DevBuf* d : all)
         if (d->p) (void)hipFree(d->p);
     for (int l = 0; l < RT_MAX_LANES; l++)
-        for (DevBuf* d : {&b->wave[l], &b->counters[l], &b->aq[l]})
+        for (DevBuf* d : {&b->wave[l], &b->counters[l]})
             if (d->p) (void)hipFree(d->p);
     for (int l = 0; l < RT_MAX_LANES; l++) {
         if (b->h_act[l]) (void)hipHostFree(b->h_act[l]);
@@ -1796,7 +1406,6 @@ struct WaveLane {
     long live = 0;  // live paths at the last readback (an upper bound: paths only finish)
     bool done = false, tail_next = false;
     int await = 0;  // 0 none, 1 live count, 2 fallback counts (tail entry check)
-    bool async = false;  // the lane's tail ran as k_async (its abort flag is read back at the end)
     hipEvent_t (*tev)[RT_MAX_TIMED_ITERS] = nullptr;  // [3][RT_MAX_TIMED_ITERS]
 };
 
@@ -1854,22 +1463,7 @@ int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounces, cons
     // profiles/r03_tail_enter4.json)
     double tail_enter = nl == 4 ? 1.4 : 2.0;
     if (const char* e = getenv("RT_TAIL_ENTER")) tail_enter = atof(e);  // (sweeps)
-    // k_async (RT_ASYNC=1; else k_tail) in place of the tail kernel (RT_TAIL_PATHS=0: neither), entered
-    // once a lane's live count is at most RT_ASYNC_ENTER; RT_ASYNC_LIMIT_S: seconds a launch may run
-    // before it gives up
-    int use_async = 0;
-    if (const char* e = getenv("RT_ASYNC")) use_async = atoi(e) != 0;
-    long async_enter = 16384;
-    if (const char* e = getenv("RT_ASYNC_ENTER")) async_enter = std::max(1l, atol(e));
-    int async_share = 1;  // RT_ASYNC_SHARE: grid-fills of a k_async launch, split over the lanes
-    int async_step_every = 4, async_calls = 2, async_refill = 4;  // RT_ASYNC_STEP_EVERY / _CALLS / _REFILL (AsyncQ)
-    if (const char* e = getenv("RT_ASYNC_STEP_EVERY")) async_step_every = std::max(2, atoi(e));
-    if (const char* e = getenv("RT_ASYNC_CALLS")) async_calls = std::max(1, atoi(e));
-    if (const char* e = getenv("RT_ASYNC_REFILL")) async_refill = std::min(16, std::max(1, atoi(e)));
-    if (const char* e = getenv("RT_ASYNC_SHARE")) async_share = std::min(4, std::max(1, atoi(e)));
-    double async_limit_s = 60.0;
-    if (const char* e = getenv("RT_ASYNC_LIMIT_S")) async_limit_s = std::max(0.001, atof(e));
-    const long tail_max = tail_p == 0 ? 0 : use_async ? async_enter : (long)(tail_enter * tail_blocks * 4 * tail_p / nl);
+    const long tail_max = (long)(tail_enter * tail_blocks * 4 * tail_p / nl);
     if (nl > 1) {
         HIPCHK(c, hipEventRecord(b->ev_fork, s));
         for (int l = 1; l < nl; l++) HIPCHK(c, hipStreamWaitEvent(b->ls[l], b->ev_fork, 0));
@@ -1994,55 +1588,6 @@ int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounces, cons
         La.await = 1;
         return RT_OK;
     };
-    // k_async's queues for lane La, sized by its live count at entry (an upper bound), cleared,
-    // then the launch; its abort flag is read back behind it (checked at the end of the render)
-    auto launch_async = [&](WaveLane& La, int par) -> int {
-        const int l = (int)(&La - L);
-        auto pow2 = [](long v) {
-            uint32_t x = 1;
-            while ((long)x < v) x <<= 1;
-            return x;
-        };
-        // per XCD: room for every live path (RQ) / 8 queries per live path (QQ) and more, so a
-        // slot is never reused while a taker may still read it
-        const uint32_t rq_n = pow2(std::max(La.live, 1l << 16)), qq_n = pow2(std::max(2 * La.live, 1l << 17));
-        const size_t o_rq = (size_t)A_COUNT * 4, o_qq = o_rq + (size_t)8 * rq_n * 8,
-                     o_seq = o_qq + (size_t)8 * qq_n * sizeof(rtk::RayRec);
-        const size_t o_pend = o_seq + (size_t)8 * qq_n * 4, bytes = o_pend + (size_t)La.n * 4;
-        if (int r = ensure(c, b->aq[l], bytes)) return r;
-        char* base = (char*)b->aq[l].p;
-        AsyncQ A;
-        A.ctr = (uint32_t*)base;
-        A.rq = (uint64_t*)(base + o_rq);
-        A.qq = (rtk::RayRec*)(base + o_qq);
-        A.qq_seq = (uint32_t*)(base + o_seq);
-        A.pend = (int32_t*)(base + o_pend);
-        A.rq_mask = rq_n - 1;
-        A.qq_mask = qq_n - 1;
-        A.limit = (long long)(async_limit_s * 1e8);
-        A.prof = nullptr;
-        A.step_every = async_step_every;
-        A.calls = async_calls;
-        A.refill = async_refill;
-        if (getenv("RT_ASYNC_PROF")) {
-            if (int r = ensure(c, b->aprof, 64 * 8 * RT_MAX_LANES)) return r;
-            A.prof = (unsigned long long*)b->aprof.p + 64 * l;
-            HIPCHK(c, hipMemsetAsync(A.prof, 0, 64 * 8, La.s));
-        }
-        HIPCHK(c, hipMemsetAsync(base, 0, o_qq, La.s));  // counters and the RQ's sequence words
-        HIPCHK(c, hipMemsetAsync(A.qq_seq, 0, (size_t)8 * qq_n * 4, La.s));
-        // (a lane's share of one grid-fill: the lanes' launches run side by side; one holding
-        // every slot would keep the others' from starting)
-        const int ab = std::max(64, tail_blocks * async_share / nl);
-        if (S)
-            hipLaunchKernelGGL(k_async<true>, dim3(ab), dim3(threads), 0, La.s, La.W, par, stats, A);
-        else
-            hipLaunchKernelGGL(k_async<false>, dim3(ab), dim3(threads), 0, La.s, La.W, par, stats, A);
-        HIPCHK(c, hipGetLastError());
-        HIPCHK(c, hipMemcpyAsync(La.h + act_bytes / 4 + 8, A.ctr + A_ABORT, 4, hipMemcpyDeviceToHost, La.s));
-        La.async = true;
-        return RT_OK;
-    };
     // enqueue up to 8 iterations, then a readback
     auto issue = [&](WaveLane& La) -> int {
         for (int k = 0; k < 8 && La.it < max_iters; k++) {
@@ -2068,15 +1613,11 @@ int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounces, cons
             if (f[C_FBC0 + par] == 0 && f[C_FBA0 + par] == 0 && f[C_PARKC0 + (par ^ 1)] == 0 &&
                 f[C_PARKA0 + (par ^ 1)] == 0) {  // (k_trace(i) released DONE[par ^ 1])
                 // few paths left and none waits: the tail kernel finishes them all
-                if (use_async) {
-                    if (int r = launch_async(La, par)) return r;
-                } else {
-                    HIPCHK(c, hipMemsetAsync(La.cnt + C_TK_TAIL, 0, 4, La.s));
-                    if (S)
-                        hipLaunchKernelGGL(k_tail<true>, dim3(tail_blocks), dim3(threads), 0, La.s, La.W, par, stats);
-                    else
-                        hipLaunchKernelGGL(k_tail<false>, dim3(tail_blocks), dim3(threads), 0, La.s, La.W, par, stats);
-                }
+                HIPCHK(c, hipMemsetAsync(La.cnt + C_TK_TAIL, 0, 4, La.s));
+                if (S)
+                    hipLaunchKernelGGL(k_tail<true>, dim3(tail_blocks), dim3(threads), 0, La.s, La.W, par, stats);
+                else
+                    hipLaunchKernelGGL(k_tail<false>, dim3(tail_blocks), dim3(threads), 0, La.s, La.W, par, stats);
                 if (b->timing && La.it < RT_MAX_TIMED_ITERS) HIPCHK(c, hipEventRecord(La.tev[2][La.it], La.s));
                 HIPCHK(c, hipGetLastError());
                 La.tail_iter = La.it;
@@ -2130,31 +1671,6 @@ int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounces, cons
     b->tail_iter = L[0].tail_iter;
     HIPCHK(c, hipEventRecord(b->ev_done, s));
     b->done_recorded = true;
-    bool any_async = false;
-    for (int l = 0; l < nl; l++) any_async = any_async || L[l].async;
-    if (any_async) {  // a k_async launch that ran out of time left paths unfinished: fail loudly
-        HIPCHK(c, hipStreamSynchronize(s));
-        if (getenv("RT_ASYNC_PROF") && b->aprof.p) {
-            unsigned long long h[64 * RT_MAX_LANES];
-            HIPCHK(c, hipMemcpy(h, b->aprof.p, sizeof(h), hipMemcpyDeviceToHost));
-            for (int l = 0; l < nl; l++) {
-                const unsigned long long* v = h + 64 * l;
-                fprintf(stderr,
-                        "[rt async] lane %d: stepper waves %llu loops %llu idle %llu steps %llu paths %llu (%.1f per step) "
-                        "step us %.1f; walker waves %llu loops %llu idle %llu visits %llu taken %llu; mean wave life us "
-                        "S %.0f W %.0f\n",
-                        l, v[AP_WAVES_S], v[AP_SLOOPS], v[AP_SIDLE], v[AP_STEPS], v[AP_PATHS],
-                        v[AP_STEPS] ? (double)v[AP_PATHS] / v[AP_STEPS] : 0.0,
-                        v[AP_STEPS] ? v[AP_STEP_TICKS] / 100.0 / v[AP_STEPS] : 0.0, v[AP_WAVES_W], v[AP_WLOOPS],
-                        v[AP_WIDLE], v[AP_VISITS], v[AP_TAKEN], v[AP_WAVES_S] ? v[AP_S_TICKS] / 100.0 / v[AP_WAVES_S] : 0.0,
-                        v[AP_WAVES_W] ? v[AP_W_TICKS] / 100.0 / v[AP_WAVES_W] : 0.0);
-            }
-        }
-        for (int l = 0; l < nl; l++)
-            if (L[l].async && L[l].h[act_bytes / 4 + 8] != 0)
-                return rt_fail(c, RT_ERR_STATE, "render: the async tail kernel (k_async) did not finish in " +
-                                                    std::to_string(async_limit_s) + " s (RT_ASYNC_LIMIT_S)");
-    }
     if (S && iter_log) {
         std::vector<int32_t> hq((size_t)6 * RT_MAX_TIMED_ITERS);
         HIPCHK(c, hipMemcpyAsync(hq.data(), b->iterq.p, hq.size() * 4, hipMemcpyDeviceToHost, s));

@@ -275,9 +275,7 @@ def test_gpu_schedules_bit_identical(monkeypatch):
     sky = scenes.make_sky("L")
     W, H, spp, nb = 640, 480, 2, 8
 
-    def render(lanes, tail, off=0, stride=1, heavy=6, enter=2.0, spec_cam=1, async_enter=0):
-        monkeypatch.setenv("RT_ASYNC", "1" if async_enter else "0")
-        monkeypatch.setenv("RT_ASYNC_ENTER", str(async_enter or 1))
+    def render(lanes, tail, off=0, stride=1, heavy=6, enter=2.0, spec_cam=1):
         monkeypatch.setenv("RT_LANES", str(lanes))
         monkeypatch.setenv("RT_TAIL_PATHS", str(tail))
         monkeypatch.setenv("RT_HEAVY", str(heavy))
@@ -315,11 +313,6 @@ def test_gpu_schedules_bit_identical(monkeypatch):
     for lanes, tail in ((1, 0), (3, 2)):
         got = render(lanes, tail, spec_cam=0)
         np.testing.assert_array_equal(got.view(np.uint32), base.view(np.uint32), err_msg=f"spec_cam=0 lanes={lanes}")
-    # the async tail kernel (k_async, opt-in), entered late and at once, on one and three lanes
-    for lanes, async_enter in ((1, 4096), (3, 1 << 30), (1, 1 << 30)):
-        got = render(lanes, 2, async_enter=async_enter)
-        np.testing.assert_array_equal(got.view(np.uint32), base.view(np.uint32),
-                                      err_msg=f"k_async lanes={lanes} enter={async_enter}")
 
 
 @pytest.mark.gpu
@@ -331,7 +324,7 @@ def test_gpu_tiny_scenes_match_oracle(n, cameras):
     assert_parity(got, want, min_bitwise=1.0)
 
 
-@pytest.mark.parametrize("tail", ["0", "5", "async"])
+@pytest.mark.parametrize("tail", ["0", "5"])
 @pytest.mark.parametrize("name,budget,every", [("mis_512", 1, 7), ("cornell32_128", 1, 7), ("cfg2_dragon", 8, 31)])
 def test_gpu_parked_walks_small_launches(name, budget, every, tail, manifest, cameras, monkeypatch):
     """Exact-walk hand-off under stress: every `every`-th query (by
@@ -343,8 +336,7 @@ def test_gpu_parked_walks_small_launches(name, budget, every, tail, manifest, ca
     (with it on, k_tail walks them inline). Every pixel must still be written,
     bit for bit the reference's."""
     monkeypatch.setenv("RT_STEP_BUDGET", str(budget))
-    monkeypatch.setenv("RT_TAIL_PATHS", "2" if tail == "async" else tail)
-    monkeypatch.setenv("RT_ASYNC", "1" if tail == "async" else "0")  # (k_async: its walkers' inline exact walks)
+    monkeypatch.setenv("RT_TAIL_PATHS", tail)
     monkeypatch.setenv("RT_FORCE_FALLBACK", str(every))
     e = rt_cases.golden_case(name, manifest)
     rk, fb = rt_cases.make_kernel(e, cameras, hostsim=False)
