@@ -80,3 +80,29 @@ build/shim_test: tests/native/shim_test.cpp include/render_kernel_hip.h include/
 	  $(REFOBJ)/bvh.o $(REFOBJ)/flattened_bvh.o $(REFOBJ)/triangle.o $(REFOBJ)/vec.o $(REFOBJ)/color.o \
 	  $(REFOBJ)/mat.o $(REFOBJ)/camera.o $(REFOBJ)/ray.o $(REFOBJ)/utils.o -Wl,--gc-sections \
 	  -L$(LIB) -lrt_hostsim -Wl,-rpath,'$$ORIGIN/../$(LIB)' -o $@
+
+# Host sanitizers: the hostsim build of the render path + the CPU oracle +
+# tests/native/sanitize_driver.cpp in one executable per sanitizer.
+#   make sanitize  -> build/sanitize_asan (ASan + UBSan) and build/sanitize_tsan (TSan), run
+#                     both; logs in profiles/r04_sanitize_{asan,tsan}.log
+# TSan: libgomp is not TSan-instrumented (its barriers would be reported as races), so the
+# TSan run uses one OpenMP thread per region; what it checks is the std::thread layer of the
+# multi-device driver (rt_for_devices, rt_render_variants) and the shared context state.
+SAN_SRCS := $(SRC)/rt_hostsim.cpp $(SRC)/rt_scene.cpp $(SRC)/rt_imageio.cpp $(SRC)/rt_capi_host.cpp
+SAN_NUM := -ffp-contract=off -fno-fast-math -fno-omit-frame-pointer -g -O1 -fopenmp
+ASAN := -fsanitize=address,undefined -fno-sanitize-recover=undefined
+TSAN := -fsanitize=thread
+
+build/san_%/driver: tests/native/sanitize_driver.cpp oracle/cpu_oracle.cpp $(SAN_SRCS) $(HDRS)
+	@mkdir -p build/san_$*
+	for f in $(SAN_SRCS); do $(CXX) -std=c++17 $(SAN_NUM) $($(shell echo $* | tr a-z A-Z)) -c $$f -o build/san_$*/$$(basename $$f .cpp).o || exit 1; done
+	$(CXX) -std=gnu++20 $(SAN_NUM) $($(shell echo $* | tr a-z A-Z)) -c oracle/cpu_oracle.cpp -o build/san_$*/cpu_oracle.o
+	$(CXX) -std=c++17 $(SAN_NUM) $($(shell echo $* | tr a-z A-Z)) tests/native/sanitize_driver.cpp build/san_$*/*.o -o $@
+
+sanitize: build/san_asan/driver build/san_tsan/driver
+	ASAN_OPTIONS=halt_on_error=1:detect_leaks=1 UBSAN_OPTIONS=print_stacktrace=1:halt_on_error=1 \
+	  OMP_NUM_THREADS=4 build/san_asan/driver scenes asan 2>&1 | tee profiles/r04_sanitize_asan.log
+	TSAN_OPTIONS=halt_on_error=1:second_deadlock_stack=1 OMP_NUM_THREADS=1 \
+	  build/san_tsan/driver scenes tsan 2>&1 | tee profiles/r04_sanitize_tsan.log
+
+.PHONY: sanitize

@@ -59,6 +59,15 @@ int rt_create(int device, rt_context** out);
  * librccl.so.1 is missing. */
 int rt_create_multi(int n_devices, const int* devices, rt_context** out);
 int rt_device_count(const rt_context* ctx);
+/* TEST ONLY (no reference counterpart). rt_create_multi_loopback: as
+ * rt_create_multi, but devices[] may name one GPU more than once and the
+ * shards are exchanged by device copies instead of RCCL, so the whole
+ * multi-device driver (threads, streams, pack / un-permute) runs on a
+ * one-GPU box. rt_test_fail_device: every later multi-device render of ctx
+ * fails device d (0..n-1) before its work starts (-1: off), to exercise the
+ * per-device error slots. Never called by the product paths. */
+int rt_create_multi_loopback(int n_devices, const int* devices, rt_context** out);
+int rt_test_fail_device(rt_context* ctx, int device);
 void rt_destroy(rt_context* ctx);
 const char* rt_last_error(const rt_context* ctx); /* ctx may be NULL: last global error */
 int rt_version(void);

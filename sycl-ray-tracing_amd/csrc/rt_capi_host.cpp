@@ -110,17 +110,18 @@ int rt_create(int device, rt_context** out)
     return RT_OK;
 }
 
-int rt_create_multi(int n_devices, const int* devices, rt_context** out)
+}  // extern "C"
+
+namespace {
+// ids: non-negative and distinct (one rank per GPU in the RCCL clique); the range is
+// checked against the devices present when the backend opens them (RT_ERR_NODEV).
+// loopback (rt_create_multi_loopback, tests only) admits a list that names a GPU more
+// than once: the context then exchanges the shards with device copies instead of RCCL.
+int create_multi(int n_devices, const int* devices, bool loopback, rt_context** out)
 {
     if (!out) return rt_fail(nullptr, RT_ERR_ARG, "rt_create_multi: out is NULL");
     *out = nullptr;
     if (n_devices < 1 || n_devices > 64) return rt_fail(nullptr, RT_ERR_ARG, "rt_create_multi: n_devices must be 1..64");
-    // ids: non-negative and distinct (one rank per GPU in the RCCL clique); the range is
-    // checked against the devices present when the backend opens them (RT_ERR_NODEV).
-    // RT_MULTI_LOOPBACK=1 (test knob) admits a list that names a GPU more than once: the
-    // context then exchanges the shards with device copies instead of RCCL, so the
-    // multi-device driver (threads, streams, pack / un-permute) runs on a one-GPU box.
-    const bool loopback = std::getenv("RT_MULTI_LOOPBACK") && std::atoi(std::getenv("RT_MULTI_LOOPBACK")) != 0;
     for (int d = 0; d < n_devices; d++) {
         const int id = devices ? devices[d] : d;
         if (id < 0) return rt_fail(nullptr, RT_ERR_ARG, "rt_create_multi: negative device id");
@@ -140,6 +141,25 @@ int rt_create_multi(int n_devices, const int* devices, rt_context** out)
         return r;
     }
     *out = c;
+    return RT_OK;
+}
+}  // namespace
+
+extern "C" {
+int rt_create_multi(int n_devices, const int* devices, rt_context** out)
+{
+    return create_multi(n_devices, devices, false, out);
+}
+
+int rt_create_multi_loopback(int n_devices, const int* devices, rt_context** out)
+{
+    return create_multi(n_devices, devices, true, out);
+}
+
+int rt_test_fail_device(rt_context* c, int device)
+{
+    if (!c) return rt_fail(nullptr, RT_ERR_ARG, "rt_test_fail_device: ctx is NULL");
+    c->fail_device = device;
     return RT_OK;
 }
 

@@ -21,6 +21,7 @@ struct rt_context {
     // One entry: a single-device context on that ordinal (nothing to shard, no RCCL)
     std::vector<int> devices;
     bool loopback = false;        // devices may repeat: shards exchanged by device copies, not RCCL
+    int fail_device = -1;         // rt_test_fail_device (tests only): that device fails its share
     std::string err;
 
     // RenderKernel constructor inputs (render_kernel.h:27-34)
@@ -80,17 +81,16 @@ void rt_err_sink(std::string* sink);
 // fn(d) for every device d of a multi-device render: d >= 1 on threads of their own,
 // d = 0 on the caller's. Each device's errors go to its own slot; after the join the
 // lowest failing device's code and message are raised on the context (one writer).
-// RT_FAIL_DEVICE=d (test knob) fails device d before its work starts.
+// c->fail_device (rt_test_fail_device, tests only) fails that device before its work starts.
 template <class F>
 int rt_for_devices(rt_context* c, int n, F fn)
 {
     std::vector<int> rc(n, 0);
     std::vector<std::string> msg(n);
-    int inject = -1;
-    if (const char* e = std::getenv("RT_FAIL_DEVICE")) inject = std::atoi(e);
+    const int inject = c->fail_device;
     auto one = [&](int d) {
         rt_err_sink(&msg[d]);
-        rc[d] = d == inject ? rt_fail(c, RT_ERR_STATE, "injected failure (RT_FAIL_DEVICE)") : fn(d);
+        rc[d] = d == inject ? rt_fail(c, RT_ERR_STATE, "injected failure (rt_test_fail_device)") : fn(d);
         rt_err_sink(nullptr);
     };
     {

@@ -8,6 +8,7 @@
 // librt_hip.so has no CPU path and fails loudly without a device.
 #include <omp.h>
 
+#include <algorithm>
 #include <cstdlib>
 #include <cstring>
 #include <vector>
@@ -32,12 +33,22 @@ int rt_backend_create(rt_context*) { return RT_OK; }
 void rt_backend_destroy(rt_context*) {}
 int rt_backend_upload(rt_context*) { return RT_OK; }
 
+// adds the per-thread counters into out (callers zero it once per render: a variant sweep sums)
 static void merge_stats(unsigned long long* out, const std::vector<rtk::Stats>& s)
 {
-    for (int i = 0; i < RT_STAT_COUNT; i++) out[i] = 0;
     for (const auto& t : s)
         for (int i = 0; i < RT_STAT_COUNT; i++) out[i] += t.c[i];
 }
+
+// The OpenMP team of one "device" thread of a multi-device render: the caller's thread
+// count split over the N devices (each device thread runs its own parallel regions), and
+// the caller's own setting restored afterwards (device 0 runs on the caller's thread).
+struct OmpShare {
+    int all, each;
+    explicit OmpShare(int n) : all(omp_get_max_threads()), each(std::max(1, omp_get_max_threads() / std::max(1, n))) {}
+    void enter() const { omp_set_num_threads(each); }
+    ~OmpShare() { omp_set_num_threads(all); }
+};
 
 // The product's wavefront loop (rt_render.hip run_wave) on the host:
 // same stage functions, same queues; appends are plain atomics.
@@ -252,11 +263,15 @@ static int render_shard(rt_context* c, int w, int h, int spp, int bounces, int o
     const int N = c->devices.empty() ? 1 : (int)c->devices.size();
     if (N == 1) {
         rtk::PixSrc src{w, off, stride, nullptr};
+        std::fill(c->stats, c->stats + RT_STAT_COUNT, 0ull);
         return run_wave_host(c, w, h, spp, bounces, src, rows * w, shard, c->stats);
     }
-    // one host thread per "device", as render_multi (rt_for_devices: per-device error slots)
+    // one host thread per "device", as render_multi (rt_for_devices: per-device error slots),
+    // each with its share of the OpenMP threads (not a full team per device)
     std::vector<std::vector<unsigned long long>> dst(N, std::vector<unsigned long long>(RT_STAT_COUNT, 0));
+    const OmpShare share(N);
     const int r = rt_for_devices(c, N, [&](int d) {
+        share.enter();
         const int rows_d = rows > d ? (rows - d + N - 1) / N : 0;
         std::vector<float4_> blk((size_t)rows_d * w);
         for (int k = 0; k < rows_d; k++) std::memcpy(&blk[(size_t)k * w], shard + (size_t)(d + k * N) * w, 16 * (size_t)w);
@@ -308,7 +323,9 @@ int rt_backend_render_variants(rt_context* c, int w, int h, int spp, int bounces
     const size_t npx = (size_t)rows * w;
     const double t0 = omp_get_wtime();
     std::vector<std::vector<unsigned long long>> dst(N, std::vector<unsigned long long>(RT_STAT_COUNT, 0));
+    const OmpShare share(N);
     const int r = rt_for_devices(c, N, [&](int d) {
+        share.enter();
         for (int v = d; v < n_var; v += N) {
             // (hostsim: the per-variant mats pointer must cover the context's material indices)
             std::vector<RtMat> tab(tabs.begin() + (size_t)v * n_mats, tabs.begin() + (size_t)(v + 1) * n_mats);
@@ -330,6 +347,7 @@ int rt_backend_render_variants(rt_context* c, int w, int h, int spp, int bounces
 int rt_backend_render_pixels(rt_context* c, int w, int h, int spp, int bounces, const int* xy, int n, float* rgba)
 {
     rtk::PixSrc src{w, 0, 1, xy};
+    std::fill(c->stats, c->stats + RT_STAT_COUNT, 0ull);
     return run_wave_host(c, w, h, spp, bounces, src, n, (float4_*)rgba, c->stats);
 }
 
@@ -366,6 +384,7 @@ int rt_backend_intersect(rt_context* c, const float* rays, int n, void* out)
             std::memcpy(o + 10, &neg1, 4);
         }
     }
+    std::fill(c->stats, c->stats + RT_STAT_COUNT, 0ull);
     merge_stats(c->stats, st);
     return RT_OK;
 }

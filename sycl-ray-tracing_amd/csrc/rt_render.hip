@@ -148,6 +148,7 @@ __host__ __device__ __forceinline__ int seg_counter(int par, int j)
 
 struct Backend {
     int device = 0;
+    int index = 0;    // position in the context's device list (0: the root)
     hipStream_t own = nullptr;  // device-side work not on a caller's stream (multi-device shards, pixel lists)
     DevBuf nodes, tri4, prim2k, mat_idx, mats, emissive, spheres, env, env_lum, cdf;
     DevBuf bvh4, bvh_tri4, parent, leaf_of, cdf_row, cdf_coarse, cdf_fence, matk;
@@ -1333,7 +1334,10 @@ int rt_backend_create(rt_context* c)
     for (int d : ids) {
         Backend* b = nullptr;
         const int r = create_one(c, d, &b);
-        if (b) g->dev.push_back(b);
+        if (b) {
+            b->index = (int)g->dev.size();
+            g->dev.push_back(b);
+        }
         if (r) return r;
     }
     if (g->multi) g->shard.resize(ids.size());
@@ -1704,16 +1708,24 @@ int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounces, cons
         // RT_TIMELINE=file: every lane's launches on one clock (ms from lane 0's first
         // k_trace): lane, iteration, k_trace start, k_trace end = k_step start, k_step end,
         // 1 for the tail kernel (tools/timeline.py)
-        if (const char* tl = getenv("RT_TIMELINE"))
-            if (FILE* f = fopen(tl, "w")) {
-                for (int l = 0; l < nl; l++)
-                    for (int i = 0; i < L[l].it && i < RT_MAX_TIMED_ITERS; i++) {
-                        float t[3];
-                        for (int k = 0; k < 3; k++) HIPCHK(c, hipEventElapsedTime(&t[k], L[0].tev[0][0], L[l].tev[k][i]));
-                        fprintf(f, "%d %d %.4f %.4f %.4f %d\n", l, i, t[0], t[1], t[2], i == L[l].tail_iter ? 1 : 0);
-                    }
+        // (device index d > 0 of a multi-device context writes file.d: the device threads run concurrently)
+        if (const char* tl = getenv("RT_TIMELINE")) {
+            std::string rows;
+            char line[128];
+            for (int l = 0; l < nl; l++)
+                for (int i = 0; i < L[l].it && i < RT_MAX_TIMED_ITERS; i++) {
+                    float t[3];
+                    for (int k = 0; k < 3; k++) HIPCHK(c, hipEventElapsedTime(&t[k], L[0].tev[0][0], L[l].tev[k][i]));
+                    snprintf(line, sizeof line, "%d %d %.4f %.4f %.4f %d\n", l, i, t[0], t[1], t[2],
+                             i == L[l].tail_iter ? 1 : 0);
+                    rows += line;
+                }
+            const std::string path = b->index > 0 ? std::string(tl) + "." + std::to_string(b->index) : std::string(tl);
+            if (FILE* f = fopen(path.c_str(), "w")) {
+                fwrite(rows.data(), 1, rows.size(), f);
                 fclose(f);
             }
+        }
     }
     return RT_OK;
 }
@@ -1874,6 +1886,8 @@ int rt_backend_render_variants(rt_context* c, int w, int h, int spp, int bounces
     const size_t npx = (size_t)rows * w;
     if (npx > 0x7fffffff / 8) return rt_fail(c, RT_ERR_ARG, "render: too many pixels for one launch");
     std::vector<float> ms(N, 0.0f);
+    // counters summed over every variant of every device (run_wave zeroes a device's per render)
+    std::vector<std::vector<unsigned long long>> vsum(N, std::vector<unsigned long long>(2 * RT_STAT_COUNT, 0));
     const int r = rt_for_devices(c, N, [&](int d) -> int {
         Backend* b = g->dev[d];
         HIPCHK(c, hipSetDevice(b->device));
@@ -1898,6 +1912,12 @@ int rt_backend_render_variants(rt_context* c, int w, int h, int spp, int bounces
             if (int e = run_wave(c, b, w, h, spp, bounces, src, (int)npx, fb, s)) return e;
             if (host_fb)
                 HIPCHK(c, hipMemcpyAsync(host_fb + 4 * npx * v, fb, npx * sizeof(float4_), hipMemcpyDeviceToHost, s));
+            if (c->stats_enabled) {  // (diagnostic renders: this variant's counters, before the next zeroes them)
+                unsigned long long one[2 * RT_STAT_COUNT];
+                HIPCHK(c, hipMemcpyAsync(one, b->stats.p, sizeof one, hipMemcpyDeviceToHost, s));
+                HIPCHK(c, hipStreamSynchronize(s));
+                for (int i = 0; i < 2 * RT_STAT_COUNT; i++) vsum[d][i] += one[i];
+            }
         }
         HIPCHK(c, hipEventRecord(b->ev1, s));
         HIPCHK(c, hipStreamSynchronize(s));
@@ -1909,16 +1929,11 @@ int rt_backend_render_variants(rt_context* c, int w, int h, int spp, int bounces
     HIPCHK(c, hipSetDevice(be(c)->device));
     if (r) return r;
     c->last_kernel_ms = *std::max_element(ms.begin(), ms.end());
-    if (c->stats_enabled) {  // (the last variant of each device, summed)
-        unsigned long long sum[2 * RT_STAT_COUNT] = {};
-        for (Backend* b : g->dev) {
-            HIPCHK(c, hipSetDevice(b->device));
-            HIPCHK(c, hipMemcpy(c->stats, b->stats.p, sizeof(c->stats), hipMemcpyDeviceToHost));
-            for (int i = 0; i < 2 * RT_STAT_COUNT; i++) sum[i] += c->stats[i];
+    if (c->stats_enabled)  // every variant of every device, summed
+        for (int i = 0; i < 2 * RT_STAT_COUNT; i++) {
+            c->stats[i] = 0;
+            for (int d = 0; d < N; d++) c->stats[i] += vsum[d][i];
         }
-        std::memcpy(c->stats, sum, sizeof sum);
-        HIPCHK(c, hipSetDevice(be(c)->device));
-    }
     return RT_OK;
 }
 

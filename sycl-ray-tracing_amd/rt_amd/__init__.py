@@ -197,15 +197,17 @@ class RenderKernel:
 
     def __init__(self, width, height, render_samples, max_bounces, image_buffer: Image, triangle_buffer,
                  materials_buffer, emissive_triangle_indices_buffer, materials_indices_buffer, analytic_spheres_buffer,
-                 bvh: BVH, skysphere: Image, env_map_cdf, device=0, hostsim: bool = False):
+                 bvh: BVH, skysphere: Image, env_map_cdf, device=0, hostsim: bool = False, loopback: bool = False):
         self.L = lib(hostsim)
         self.width, self.height = int(width), int(height)
         self.render_samples, self.max_bounces = int(render_samples), int(max_bounces)
         self.frame_buffer = image_buffer
         h = ctypes.c_void_p()
         if isinstance(device, (list, tuple)):
+            # loopback (tests / rehearsals only): the list may repeat a GPU, shards move by device copies
             ids = np.ascontiguousarray(device, dtype=np.int32)
-            check(self.L, self.L.rt_create_multi(ids.shape[0], ptr(ids), ctypes.byref(h)), None, "rt_create_multi")
+            create = self.L.rt_create_multi_loopback if loopback else self.L.rt_create_multi
+            check(self.L, create(ids.shape[0], ptr(ids), ctypes.byref(h)), None, "rt_create_multi")
         else:
             check(self.L, self.L.rt_create(int(device), ctypes.byref(h)), None, "rt_create")
         self.ctx = h
@@ -321,6 +323,10 @@ class RenderKernel:
         """USE_BVH (render_kernel.h:13): False switches INTERSECT_SCENE to the
         brute-force intersect_scene loop (render_kernel.cpp:453-483)."""
         check(self.L, self.L.rt_set_intersect_mode(self.ctx, 1 if use_bvh else 0), self.ctx, "rt_set_intersect_mode")
+
+    def test_fail_device(self, device: int = -1):
+        """Tests only (rt_test_fail_device): later multi-device renders fail `device` (-1: off)."""
+        check(self.L, self.L.rt_test_fail_device(self.ctx, int(device)), self.ctx, "rt_test_fail_device")
 
     def set_stats(self, on: bool):
         self.L.rt_set_stats(self.ctx, 1 if on else 0)

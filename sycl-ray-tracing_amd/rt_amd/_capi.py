@@ -24,6 +24,7 @@ EXPORTS = [
     "rt_mesh_load", "rt_mesh_counts", "rt_mesh_copy", "rt_mesh_free", "rt_camera_preset", "rt_env_luminance_cdf",
     "rt_octree_dump", "rt_read_hdr", "rt_write_png", "rt_image_to_rgba8",
     "rt_set_intersect_mode", "rt_create_multi", "rt_device_count", "rt_set_materials", "rt_render_variants",
+    "rt_create_multi_loopback", "rt_test_fail_device",
 ]
 
 # return codes (include/rt_hip.h)
@@ -37,6 +38,8 @@ F = ctypes.c_float
 _SIGS = {
     "rt_create": (I, [I, ctypes.POINTER(P)]),
     "rt_create_multi": (I, [I, P, ctypes.POINTER(P)]),
+    "rt_create_multi_loopback": (I, [I, P, ctypes.POINTER(P)]),
+    "rt_test_fail_device": (I, [P, I]),
     "rt_device_count": (I, [P]),
     "rt_set_materials": (I, [P, P, I]),
     "rt_destroy": (None, [P]),

@@ -6,8 +6,8 @@ table pushed alone (rt_set_materials, the reference's by-reference
 CPU: the hostsim build shards the same way (one host thread per device, host
 copies in place of RCCL), so the row mapping, the per-device error collection
 and recovery are checked here against the reference's goldens. GPU: the
-multi-device driver on one GPU through its loopback exchange (RT_MULTI_LOOPBACK:
-device copies in place of RCCL, which needs distinct GPUs) and the cfg5 material
+multi-device driver on one GPU through its loopback exchange (rt_create_multi_loopback,
+a test-only entry: device copies in place of RCCL, which needs distinct GPUs) and the cfg5 material
 sweep through one context, against the compiled reference's goldens. The RCCL
 scatter / gather itself runs only on a node with two or more GPUs (bench.py
 --gpus N, the driver's scaling runs)."""
@@ -50,31 +50,33 @@ def test_hostsim_multi_device_shard_matches_golden(n, off, stride, manifest, cam
 
 
 @pytest.mark.parametrize("bad", [1, 2])
-def test_hostsim_multi_device_failure_surfaces_and_recovers(bad, manifest, cameras, monkeypatch):
-    """A device >= 1 failing inside a multi-device render (RT_FAIL_DEVICE test knob):
+def test_hostsim_multi_device_failure_surfaces_and_recovers(bad, manifest, cameras):
+    """A device >= 1 failing inside a multi-device render (rt_test_fail_device, tests only):
     the render returns its error code with the device's message (collected in the
     device thread's own slot, raised once after the join), and the next render on
     the same context succeeds bit for bit."""
     e = rt_cases.golden_case("cornell32_128", manifest)
     rk, fb = rt_cases.make_kernel(e, cameras, hostsim=True, device=[0, 1, 2])
-    monkeypatch.setenv("RT_FAIL_DEVICE", str(bad))
+    rk.test_fail_device(bad)
     with pytest.raises(rt_amd.RtError) as ei:
         rk.render()
     assert f"({rt_amd.RT_ERR_STATE})" in str(ei.value) and f"device {bad}: injected failure" in str(ei.value)
-    monkeypatch.delenv("RT_FAIL_DEVICE")
+    rk.test_fail_device(-1)
     fb.pixels[...] = rt_amd.Image(e["W"], e["H"]).pixels
     rk.render()
     np.testing.assert_array_equal(_bits(fb.pixels), _bits(e["expected"]))
 
 
 def test_create_multi_device_ids(monkeypatch):
-    """rt_create_multi: a device listed twice or a negative id is RT_ERR_ARG; one listed
-    device is a single-device context on that ordinal (nothing to shard, no RCCL)."""
+    """rt_create_multi: a device listed twice or a negative id is RT_ERR_ARG (an
+    environment variable cannot turn the check off: the loopback form is its own
+    test-only entry); one listed device is a single-device context on that ordinal
+    (nothing to shard, no RCCL)."""
     import ctypes
     from rt_amd._capi import lib
     L = lib(hostsim=True)
     h = ctypes.c_void_p()
-    monkeypatch.delenv("RT_MULTI_LOOPBACK", raising=False)
+    monkeypatch.setenv("RT_MULTI_LOOPBACK", "1")  # (the round-3 knob: no longer read)
     for ids in ([0, 0], [1, 2, 1], [-1, 0]):
         a = np.asarray(ids, np.int32)
         assert L.rt_create_multi(len(ids), a.ctypes.data_as(ctypes.c_void_p), ctypes.byref(h)) == rt_amd.RT_ERR_ARG
@@ -82,6 +84,12 @@ def test_create_multi_device_ids(monkeypatch):
     a = np.asarray([3], np.int32)
     assert L.rt_create_multi(1, a.ctypes.data_as(ctypes.c_void_p), ctypes.byref(h)) == 0
     assert L.rt_device_count(h) == 1
+    L.rt_destroy(h)
+    a = np.asarray([-1, 0], np.int32)
+    assert L.rt_create_multi_loopback(2, a.ctypes.data_as(ctypes.c_void_p), ctypes.byref(h)) == rt_amd.RT_ERR_ARG
+    a = np.asarray([0, 0], np.int32)
+    assert L.rt_create_multi_loopback(2, a.ctypes.data_as(ctypes.c_void_p), ctypes.byref(h)) == 0
+    assert L.rt_device_count(h) == 2
     L.rt_destroy(h)
 
 
@@ -135,17 +143,16 @@ def test_gpu_multi_context_one_device_is_single(manifest, cameras):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("ids", [[0, 0], [0, 0, 0]])
-def test_gpu_multi_device_driver_loopback(ids, manifest, cameras, monkeypatch):
-    """The multi-device driver on one GPU (RT_MULTI_LOOPBACK: the device list may name
+def test_gpu_multi_device_driver_loopback(ids, manifest, cameras):
+    """The multi-device driver on one GPU (rt_create_multi_loopback: the device list may name
     GPU 0 repeatedly; the shards are exchanged with device copies instead of RCCL):
     the row pack, one host thread and stream per device running its own wavefront
     loop, the block exchange and the un-permute, bit-identical to the goldens for
-    frames, row shards and the dragon; then a device failure (RT_FAIL_DEVICE) surfaces
+    frames, row shards and the dragon; then a device failure (rt_test_fail_device) surfaces
     and the context renders correctly again."""
     from hip_mem import DeviceBuffer
-    monkeypatch.setenv("RT_MULTI_LOOPBACK", "1")
     e = rt_cases.golden_case("cornell32_128", manifest)
-    rk, fb = rt_cases.make_kernel(e, cameras, hostsim=False, device=ids)
+    rk, fb = rt_cases.make_kernel(e, cameras, hostsim=False, device=ids, loopback=True)
     assert rk.n_devices == len(ids)
     rk.render()
     np.testing.assert_array_equal(_bits(fb.pixels), _bits(e["expected"]))
@@ -158,18 +165,18 @@ def test_gpu_multi_device_driver_loopback(ids, manifest, cameras, monkeypatch):
         rk.render_device(buf.ptr, off, stride, None)
         got = buf.download(init.shape, np.float32)
         np.testing.assert_array_equal(_bits(got), _bits(e["expected"][off::stride]))
-    monkeypatch.setenv("RT_FAIL_DEVICE", str(len(ids) - 1))
+    rk.test_fail_device(len(ids) - 1)
     fb.pixels[...] = rt_amd.Image(e["W"], e["H"]).pixels
     with pytest.raises(rt_amd.RtError) as ei:
         rk.render()
     assert f"device {len(ids) - 1}: injected failure" in str(ei.value)
-    monkeypatch.delenv("RT_FAIL_DEVICE")
+    rk.test_fail_device(-1)
     fb.pixels[...] = rt_amd.Image(e["W"], e["H"]).pixels
     rk.render()
     np.testing.assert_array_equal(_bits(fb.pixels), _bits(e["expected"]))
     # a dragon frame's row shard (cfg2 rows at 4 spp) against the single-device context
     g = rt_cases.golden_case("cfg2_dragon", manifest)
-    rk2, _ = rt_cases.make_kernel(g, cameras, hostsim=False, device=ids, spp=4)
+    rk2, _ = rt_cases.make_kernel(g, cameras, hostsim=False, device=ids, spp=4, loopback=True)
     rk1, _ = rt_cases.make_kernel(g, cameras, hostsim=False, device=0, spp=4)
     outs = []
     for k in (rk2, rk1):
@@ -284,18 +291,17 @@ CFG5_ROWS = (1, 539)
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("devices", [0, [0, 0]])
-def test_gpu_cfg5_variants_replicas_match_goldens(devices, manifest, cameras, monkeypatch):
+def test_gpu_cfg5_variants_replicas_match_goldens(devices, manifest, cameras):
     """BASELINE config 5 as replicas: the 16 material variants in one rt_render_variants
     call (rows 1, 540, 1079 of each 1920x1080x1024spp frame), against the compiled
     reference's goldens on every golden pixel of those rows, host and device outputs;
-    [0, 0]: two replica devices on one GPU (RT_MULTI_LOOPBACK), variants alternating."""
+    [0, 0]: two replica devices on one GPU (rt_create_multi_loopback), variants alternating."""
     from hip_mem import DeviceBuffer
-    if isinstance(devices, list):
-        monkeypatch.setenv("RT_MULTI_LOOPBACK", "1")
     cases = [rt_cases.golden_case(f"cfg5_sweep_m{m}_r{r}", manifest) for m in range(4) for r in range(4)]
     P = parsed_scene(cases[0]["scene"])
     tabs = [rt_cases.materials_for(e, P) for e in cases]
-    rk, _ = rt_cases.make_kernel(cases[0], cameras, hostsim=False, device=devices)
+    rk, _ = rt_cases.make_kernel(cases[0], cameras, hostsim=False, device=devices,
+                                 loopback=isinstance(devices, list))
     off, stride = CFG5_ROWS
     rows = list(range(off, cases[0]["H"], stride))
     frames = rk.render_variants(tabs, row_offset=off, row_stride=stride)
@@ -316,3 +322,47 @@ def test_gpu_cfg5_variants_replicas_match_goldens(devices, manifest, cameras, mo
     rk.render_variants(tabs, device_ptrs=[b.ptr for b in bufs], row_offset=off, row_stride=stride)
     for v, b in enumerate(bufs):
         np.testing.assert_array_equal(_bits(b.download(init.shape, np.float32)), _bits(frames[v]))
+
+
+def test_hostsim_render_variants_stats_cover_every_variant(manifest, cameras):
+    """rt_get_stats after rt_render_variants holds every variant's counters (summed over
+    variants and devices), not only the last variant's."""
+    e = rt_cases.golden_case("cornell32_128", manifest)
+    P = parsed_scene(e["scene"])
+    tabs = _variant_tables(P, 3)
+    per = []
+    for m in tabs:
+        ref, _ = rt_cases.make_kernel(e, cameras, hostsim=True, W=24, H=20, materials=m.copy())
+        ref.set_stats(True)
+        ref.render()
+        per.append(ref.stats())
+    for devices in (0, [0, 1]):
+        rk, _ = rt_cases.make_kernel(e, cameras, hostsim=True, device=devices, W=24, H=20)
+        rk.set_stats(True)
+        rk.render_variants(tabs)
+        got = rk.stats()
+        for k in ("rays", "any_rays", "steps", "mat"):
+            assert got[k] == sum(s[k] for s in per), (devices, k, got[k], [s[k] for s in per])
+
+
+@pytest.mark.gpu
+def test_gpu_render_after_variants_keeps_bound_table(manifest, cameras):
+    """render, rt_render_variants with tables LONGER than the bound one (more materials:
+    the n_mats / LDS material staging paths), render again: the two plain renders are
+    bitwise equal, and each variant equals a fresh context built with its table."""
+    e = rt_cases.golden_case("cornell32_128", manifest)
+    P = parsed_scene(e["scene"])
+    W, H = 48, 40
+    rk, fb = rt_cases.make_kernel(e, cameras, hostsim=False, W=W, H=H)
+    rk.render()
+    first = fb.pixels.copy()
+    extra = np.repeat(P.materials[-1:], 70, axis=0)  # 70 unused materials: > the 64-entry LDS table
+    tabs = [np.concatenate([m, extra]) for m in _variant_tables(P, 3)]
+    frames = rk.render_variants(tabs)
+    for v, m in enumerate(tabs):
+        ref, rfb = rt_cases.make_kernel(e, cameras, hostsim=False, W=W, H=H, materials=m.copy())
+        ref.render()
+        np.testing.assert_array_equal(_bits(frames[v]), _bits(rfb.pixels))
+    fb.pixels[...] = rt_amd.Image(W, H).pixels
+    rk.render()
+    np.testing.assert_array_equal(_bits(fb.pixels), _bits(first))
