@@ -38,6 +38,9 @@ $(OBJ)/rt_render.o: $(SRC)/rt_render.hip $(HDRS)
 $(LIB)/librt_hip.so: $(OBJ)/rt_render.o $(OBJ)/rt_scene.host.o $(OBJ)/rt_imageio.host.o $(OBJ)/rt_capi_host.host.o
 	@mkdir -p $(LIB)
 	$(HIPCC) -shared --offload-arch=$(ARCH) -fPIC $^ -o $@
+	@# the commit the product library was built from (+ "-dirty" with uncommitted source changes): bench.py names it
+	@(git rev-parse --short HEAD 2>/dev/null || echo unknown) | tr -d '\n' > BUILD_COMMIT; \
+	  git diff --quiet HEAD -- $(SRC) include 2>/dev/null || printf -- "-dirty" >> BUILD_COMMIT
 
 $(LIB)/librt_hostsim.so: $(OBJ)/rt_hostsim.o $(OBJ)/rt_scene.host.o $(OBJ)/rt_imageio.host.o $(OBJ)/rt_capi_host.host.o
 	@mkdir -p $(LIB)

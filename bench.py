@@ -224,6 +224,28 @@ def load_traffic(key):
     return None if e is None else e.get("bytes_per_launch")
 
 
+def build_commit():
+    """The commit librt_hip.so was built from (BUILD_COMMIT, written by `make` with the library)."""
+    try:
+        return open(os.path.join(REPO, "BUILD_COMMIT")).read().strip() or None
+    except OSError:
+        return None
+
+
+def traffic_source(key):
+    """Where the committed FETCH_SIZE figure comes from: its profile, the build it measured and
+    whether that is the build running now (profiles/traffic.json, tools/update_traffic.py)."""
+    p = os.path.join(REPO, "profiles", "traffic.json")
+    if not os.path.exists(p):
+        return None
+    e = json.load(open(p)).get(key)
+    if e is None:
+        return None
+    now = build_commit()
+    return {"profile": e.get("profile"), "build": e.get("build"), "running_build": now,
+            "same_build": bool(now and e.get("build") and now == e.get("build"))}
+
+
 def load_traffic_class(key, cls):
     """PMC FETCH_SIZE bytes per launch of one kernel class from profiles/traffic.json."""
     p = os.path.join(REPO, "profiles", "traffic.json")
@@ -352,6 +374,54 @@ def run_sweep(args, rank, world, dev, single_process_multi, torch, dist):
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    if rank == 0 and parity["bitwise_fraction"] < 1.0:
+        fail(f"PARITY FAILURE: cfg5 sweep pixels differ from the reference's goldens ({parity})", code=3)
+
+
+def frame_compare(a, b, torch) -> dict:
+    """Two frames of the same pixels (device tensors [..., 4] f32): the fraction of pixels whose
+    four channels are bit-identical (NaN bits included), per-channel L-inf on RGB with NaN ==
+    NaN, and ok = every pixel bit-identical (the multi-GPU partition must not change a bit)."""
+    a = a.reshape(-1, 4).contiguous()
+    b = b.reshape(-1, 4).contiguous()
+    same = (a.view(torch.int32) == b.view(torch.int32)).all(dim=1)
+    na, nb = torch.isnan(a[:, :3]), torch.isnan(b[:, :3])
+    both = ~(na | nb)
+    diff = torch.where(both, (a[:, :3] - b[:, :3]).abs(), torch.zeros_like(a[:, :3]))
+    nan_mismatch = int((na != nb).sum())
+    n = a.shape[0]
+    frac = float(same.float().mean()) if n else 1.0
+    return {"pixels": n, "bitwise_fraction": frac, "linf": float("inf") if nan_mismatch else
+            (float(diff.max()) if n else 0.0), "nan_mismatch": nan_mismatch, "ok": bool(n == 0 or bool(same.all()))}
+
+
+def solo_kernel(rk, P, sky, cam17, dev, single_process_multi):
+    """A single-device RenderKernel on this rank's GPU: rk itself (torchrun: one device per
+    process), or a new one when rk spans several devices (one-process multi-device context)."""
+    if not single_process_multi:
+        return rk
+    import rt_amd
+    k = rt_amd.RenderKernel(rk.width, rk.height, rk.render_samples, rk.max_bounces, rt_amd.Image(1, 1), P.triangles,
+                            P.materials, P.emissive_triangle_indices, P.material_indices, None, rt_amd.BVH(P.triangles),
+                            rt_amd.Image.from_rgb(sky), None, device=dev.index)
+    k.set_camera(rt_amd.Camera(cam17[:16], cam17[16]))
+    return k
+
+
+def multi_parity(full, solo, dev, torch, rows_every=61, first=7) -> dict:
+    """N > 1: rows first, first + rows_every, ... of the gathered N-GPU frame against the same
+    rows rendered by ONE device alone (render_kernel.cpp:189-211 writes the whole Image&, so a
+    gather that drops or permutes rows must show here). Bitwise."""
+    from rt_amd.dist import ShardedFrame
+    dev = torch.device(dev)
+    sub = ShardedFrame(solo, first, rows_every, device=dev)
+    sub.render(torch.cuda.current_stream(dev).cuda_stream if dev.type == "cuda" else None)
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+    c = frame_compare(full[first::rows_every], sub.shard[: sub.rows], torch)
+    c["against"] = (f"rows {first}::{rows_every} ({sub.rows} rows x {solo.width} px) rendered by one device alone "
+                    f"(a single-device context on {dev})")
+    return c
 
 
 def strong_cfg4(args, rk, P, sky, cam17, rank, world, dev, single_process_multi, torch, dist) -> dict:
@@ -376,18 +446,18 @@ def strong_cfg4(args, rk, P, sky, cam17, rank, world, dev, single_process_multi,
         if world > 1 and gather:
             dist.barrier()
         t0 = time.perf_counter()
+        out = None
         for _ in range(reps):
             frame.render(stream)
-            if gather:
-                frame.gather()
+            out = frame.gather() if gather else frame.shard[: frame.rows]
         torch.cuda.synchronize(dev)
         if world > 1 and gather:
             dist.barrier()
-        return (time.perf_counter() - t0) / reps
+        return (time.perf_counter() - t0) / reps, out
 
     # T_N: the split, exactly as the line's frames are split
     frame = ShardedFrame(rk, 0, 1, device=dev) if single_process_multi else ShardedFrame(rk, rank, world, device=dev)
-    tn = timed(frame, gather=True)
+    tn, full_n = timed(frame, gather=True)
     if world > 1:
         t = torch.tensor([tn], dtype=torch.float64, device=dev if dist.get_backend() == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -395,14 +465,18 @@ def strong_cfg4(args, rk, P, sky, cam17, rank, world, dev, single_process_multi,
     del frame
     rk.width, rk.height, rk.render_samples, rk.max_bounces = saved
     # T_1: the whole frame on GPU 0 alone (a single-device context; the other ranks wait)
-    t1 = None
+    t1, bitwise = None, None
     if rank == 0:
         k1 = rt_amd.RenderKernel(W4, H4, spp4, nb4, rt_amd.Image(1, 1), P.triangles, P.materials,
                                  P.emissive_triangle_indices, P.material_indices, None, rt_amd.BVH(P.triangles),
                                  rt_amd.Image.from_rgb(sky), None, device=dev.index)
         k1.set_camera(rt_amd.Camera(cam17[:16], cam17[16]))
-        t1 = timed(ShardedFrame(k1, 0, 1, device=dev), gather=False)
-        del k1
+        t1, full_1 = timed(ShardedFrame(k1, 0, 1, device=dev), gather=False)
+        # the gathered N-GPU frame against the 1-GPU frame, every pixel, bit for bit
+        bitwise = frame_compare(full_n, full_1, torch)
+        bitwise["against"] = "the same cfg4 frame rendered by GPU 0 alone (T_1's frame), every pixel"
+        del k1, full_1
+    del full_n
     if world > 1:
         dist.barrier()
     if rank != 0:
@@ -411,6 +485,7 @@ def strong_cfg4(args, rk, P, sky, cam17, rank, world, dev, single_process_multi,
             "ms_1gpu": round(t1 * 1e3, 2), "ms_n_gpus": round(tn * 1e3, 2), "n_gpus": n,
             "msamples_per_s_n_gpus": round(W4 * H4 * spp4 / tn / 1e6, 1),
             "efficiency": round(t1 / (n * tn), 4),
+            "bitwise": bitwise,
             "measured": "one render each after a warm-up; T_N = max over ranks incl. the RCCL exchange; "
                         "T_1 = the same frame on GPU 0 alone"}
 
@@ -449,7 +524,11 @@ def main():
 
     n_gpus = args.gpus
     single_process_multi = world == 1 and n_gpus > 1
-    if single_process_multi:
+    # (RT_BENCH_LOOPBACK=1: rehearse the one-process multi-device driver on one GPU — the
+    # device list repeats GPU 0 and the shards move by device copies, rt_create_multi_loopback;
+    # never set for a measurement)
+    loopback = single_process_multi and os.environ.get("RT_BENCH_LOOPBACK") == "1"
+    if single_process_multi and not loopback:
         have = torch.cuda.device_count()
         if have < n_gpus:
             fail(f"--gpus {n_gpus} but only {have} HIP device(s) visible")
@@ -477,10 +556,10 @@ def main():
     if world > 1:
         dist.barrier()
     P, sky, cam17 = build_inputs(args.config)
-    devices = list(range(n_gpus)) if single_process_multi else local
+    devices = ([0] * n_gpus if loopback else list(range(n_gpus))) if single_process_multi else local
     rk = rt_amd.RenderKernel(W, H, spp, nb, rt_amd.Image(1, 1), P.triangles, P.materials,
                              P.emissive_triangle_indices, P.material_indices, None, rt_amd.BVH(P.triangles),
-                             rt_amd.Image.from_rgb(sky), None, device=devices)
+                             rt_amd.Image.from_rgb(sky), None, device=devices, loopback=loopback)
     rk.set_camera(rt_amd.Camera(cam17[:16], cam17[16]))
     if single_process_multi:
         frame = ShardedFrame(rk, 0, 1, device=dev)  # the root's full frame; the context shards it
@@ -493,14 +572,21 @@ def main():
     stream = torch.cuda.current_stream(dev).cuda_stream
 
     # counter pass (same workload, stats kernel variant) -> algorithmic bytes
-    stats = None
+    stats, stats_seq = None, None
     if not args.no_stats:
         rk.set_stats(True)
         frame.render(stream)
         torch.cuda.synchronize(dev)
         stats = rk.stats()
-        rk.set_stats(False)
         log(f"[rank {rank}] counters {stats}  iterations {rk.last_iterations()}")
+        if n_gpus == 1:
+            # the same frame with unpaired occlusion walks: the box tests a walk must make
+            # (the product pairs the stack top's node into a trip; same answers)
+            rk.set_stats(2)
+            frame.render(stream)
+            torch.cuda.synchronize(dev)
+            stats_seq = rk.stats()
+        rk.set_stats(False)
 
     elapsed, full, kernel_ms = None, None, None
     if not args.roofline_only:
@@ -552,13 +638,26 @@ def main():
         algo = algo_bytes(stats, "trace") / max(launches, 1)  # per launch (the stats pass rendered the same frame)
         avg_ms = tot_ms / max(launches, 1)
         achieved = algo / (avg_ms * 1e-3) / 1e9
+        necessary = None
+        if stats_seq is not None:
+            necessary = algo_bytes(stats_seq, "trace") / max(launches, 1) / (avg_ms * 1e-3) / 1e9
+        tkey = f"{args.config}_1lane"
         roofline = {"bound": "hbm", "kernel": "k_trace", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                    "achieved_necessary": None if necessary is None else round(necessary, 1),
+                    "frac_necessary": None if necessary is None else round(necessary / HBM_PEAK_GBS, 4),
+                    "necessary_model": "as byte_model, but the box tests of a counter render whose occlusion walks "
+                                       "take one node per trip (rt_set_stats 2: the tests a walk must make; the "
+                                       "product's paired trips also test the stack top's node, counted in frac)",
+                    "occlusion_box_tests": None if stats_seq is None else
+                    {"executed": stats["any_vol"] - stats.get("tail_any_vol", 0),
+                     "necessary": stats_seq["any_vol"] - stats_seq.get("tail_any_vol", 0)},
                     "byte_model": "records a query must read (bench.py BYTES): 32 B per search-BVH box test (one "
                                   "child record), 48 B per triangle test, 64 B per octree verification slab test, "
                                   "40 B per query (queue ray + result); box tests counted as executed, incl. the "
                                   "paired occlusion trips' stack-top node",
-                    "traffic": load_traffic(f"{args.config}_1lane") if (n_gpus == 1 and not args.sim_world) else None,
+                    "traffic": load_traffic(tkey) if (n_gpus == 1 and not args.sim_world) else None,
+                    "traffic_source": traffic_source(tkey) if (n_gpus == 1 and not args.sim_world) else None,
                     "measured": "1-lane render after the timed steps (one stream: launches do not overlap); "
                                 "HIP events around each launch",
                     "algo_bytes_per_launch": round(algo), "avg_launch_ms": round(avg_ms, 4),
@@ -607,13 +706,25 @@ def main():
             # verification does ~5x fewer node tests than the reference's octree walk
             roofline["ref_model_rate_GBps"] = round(ref["ref_model_bytes_per_sample"] * value * 1e6 / 1e9, 1)
 
+    # N > 1: the gathered frame's rows against one device's render of the same rows (rank 0)
+    if n_gpus > 1 and not args.sim_world and full is not None and rank == 0:
+        solo = solo_kernel(rk, P, sky, cam17, dev, single_process_multi)
+        parity = multi_parity(full, solo, dev, torch)
+        if solo is not rk:
+            del solo
+    if world > 1:
+        dist.barrier()
+
     strong = None
     if n_gpus > 1 and not args.sim_world and not args.no_strong_cfg4:
         strong = strong_cfg4(args, rk, P, sky, cam17, rank, world, dev, single_process_multi, torch, dist)
     if world > 1:
         dist.barrier()
     if rank == 0:
-        if single_process_multi:
+        if loopback:
+            par = (f"REHEARSAL, not a measurement: one process, rt_create_multi_loopback over GPU 0 x {n_gpus}: "
+                   f"rows y%{n_gpus}, device-copy exchange")
+        elif single_process_multi:
             par = f"one process, rt_create_multi over {n_gpus} GPUs: rows y%{n_gpus} + RCCL scatter/gather"
         elif world > 1:
             par = f"{world} processes (torchrun): rows y%{world} per GPU + {dist.get_backend()} gather"
@@ -633,6 +744,7 @@ def main():
                                                                  else ""),
                        "W": W, "H": H, "spp": spp, "bounces": nb, "parallelism": par},
             "setup_s": round(setup_s, 2),
+            "build": build_commit(),
             "roofline": roofline,
             "cpu_baseline": cpu,
             "parity": parity,
@@ -640,8 +752,20 @@ def main():
         if strong is not None:
             out["strong_cfg4"] = strong
         print(json.dumps(out), flush=True)
+    # a frame that differs from the reference's (N = 1: the CPU port's rows, 1e-4 per channel
+    # after tone-map; N > 1: the gathered frame against one device's, bitwise) fails the run
+    bad = []
+    if rank == 0 and parity is not None:
+        if n_gpus > 1 and not parity.get("ok", False):
+            bad.append(f"gathered frame rows differ from one device's ({parity})")
+        if n_gpus == 1 and (parity["nan_mismatch"] or parity["linf"] > 1e-4):
+            bad.append(f"frame rows differ from the CPU port's ({parity})")
+    if rank == 0 and strong is not None and not strong["bitwise"]["ok"]:
+        bad.append(f"strong_cfg4: the {n_gpus}-GPU frame differs from the 1-GPU frame ({strong['bitwise']})")
     if world > 1:
         dist.destroy_process_group()
+    if bad:
+        fail("PARITY FAILURE: " + "; ".join(bad), code=3)
 
 
 if __name__ == "__main__":

@@ -152,6 +152,10 @@ int rt_set_intersect_mode(rt_context* ctx, int use_bvh);
 /* Counters of the last render when enabled (RT_STAT_* order, rt_device.h);
  * with n up to 2 * RT_STAT_COUNT the second block is the share of the
  * gfx950 tail kernel (k_tail) in those totals. */
+/* enabled = 2: counters of a render whose occlusion walks take one node per trip
+ * (the gfx950 walks otherwise pair the stack top's node into the same trip, testing
+ * boxes a one-node walk may never reach): the box tests a walk must make, for the
+ * roofline's necessary-bytes figure. Same answers, same frame. */
 int rt_set_stats(rt_context* ctx, int enabled);
 int rt_get_stats(const rt_context* ctx, unsigned long long* out, int n);
 /* Average duration (ms) of the last render kernel measured with HIP events. */

@@ -418,6 +418,7 @@ int rt_set_stats(rt_context* c, int enabled)
 {
     if (!c) return RT_ERR_ARG;
     c->stats_enabled = enabled != 0;
+    c->stats_seq = enabled == 2;
     return RT_OK;
 }
 

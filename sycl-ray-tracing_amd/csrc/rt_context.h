@@ -49,6 +49,7 @@ struct rt_context {
 
     bool brute = false;           // USE_BVH 0 (rt_set_intersect_mode)
     bool stats_enabled = false;
+    bool stats_seq = false;       // rt_set_stats(ctx, 2): occlusion walks unpaired (gfx950), see rt_hip.h
     unsigned long long stats[2 * RT_STAT_COUNT] = {};  // all kernels, then the gfx950 tail kernel's share
     double last_kernel_ms = 0.0;
 

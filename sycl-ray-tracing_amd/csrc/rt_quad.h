@@ -236,7 +236,9 @@ __device__ __forceinline__ bool qstate_begin(QState& q, V3 o, V3 d, int sub, Sta
 // -6 %, cfg4 8-way shard 411 -> 402 ms (r02). Three nodes per trip (821-824) and the
 // same pairing for closest-hit walks (710-722: the looser nearest-first order cost 25 %
 // more exact-walk fallbacks) were slower (profiles/r02_k_trace_variants.jsonl).
-template <bool ANY, int DESC = RT_VISIT_DESCEND, class QSTK>
+// PAIR = false (stats renders only, rt_set_stats(ctx, 2)): occlusion walks take one node per
+// trip, so their box-test counters are the necessary ones (answers do not depend on the order).
+template <bool ANY, int DESC = RT_VISIT_DESCEND, bool PAIR = true, class QSTK>
 __device__ __forceinline__ int quad_visit(const RtSceneView& S, QState& q, QSTK& stk, int sub, Stats* st)
 {
     FastHit& h = q.h;
@@ -244,7 +246,7 @@ __device__ __forceinline__ int quad_visit(const RtSceneView& S, QState& q, QSTK&
     for (int dd = 0; dd < DESC && q.cur >= 0; dd++) {
         if (ANY) {
             // the current node and the stack top's inner node in one trip
-            constexpr int NW = 2;
+            constexpr int NW = PAIR ? 2 : 1;
             int nd[NW];
             nd[0] = q.cur;
             int m = 1;

@@ -665,7 +665,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_STEP_OCC
 }
 
 // k_trace's fast roles with per-quad refill (RT_TRACE_REFILL > 0): see k_trace.
-template <bool ANY, bool STATS, class QSTK>
+template <bool ANY, bool STATS, bool PAIR, class QSTK>
 __device__ __forceinline__ void trace_stream(const rtk::WaveView& W, const RtSceneView& S, QSTK& stk, const int* s_pre,
                                              int first, int total, int wg, int wn, int32_t* fbn, rtk::RayRec* fbl,
                                              rtk::Stats* ps)
@@ -716,7 +716,7 @@ __device__ __forceinline__ void trace_stream(const rtk::WaveView& W, const RtSce
             if (lane == 0) ps->c[exhausted ? RT_STAT_DRAIN_SLOTS : RT_STAT_WAVE_SLOTS] += 16;
         }
         if (active) {
-            int res = rtk::quad_visit<ANY>(S, q, stk, sub, ps);
+            int res = rtk::quad_visit<ANY, RT_VISIT_DESCEND, PAIR>(S, q, stk, sub, ps);
             q.calls++;
             if (res != 0) {
                 active = false;
@@ -749,7 +749,7 @@ __device__ __forceinline__ void trace_stream(const rtk::WaveView& W, const RtSce
     }
 }
 
-template <bool STATS>
+template <bool STATS, bool PAIR = true>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_OCC, 8))) void k_trace(rtk::WaveView W, int par, unsigned long long* stats)
 {
     __shared__ uint32_t s_lds[RT_LDS_WORDS * 256];
@@ -803,9 +803,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_OC
     // RT_TRACE_REFILL quads are idle they all take the next queries, so a long walk holds
     // up its own quad, not the wave's next 15 queries.
     if (closest)
-        trace_stream<false, STATS>(W, S, stk, s_pre, c0, total, wg, wn, fbn, fbl, ps);
+        trace_stream<false, STATS, PAIR>(W, S, stk, s_pre, c0, total, wg, wn, fbn, fbl, ps);
     else
-        trace_stream<true, STATS>(W, S, stk, s_pre, a0, total, wg, wn, fbn, fbl, ps);
+        trace_stream<true, STATS, PAIR>(W, S, stk, s_pre, a0, total, wg, wn, fbn, fbl, ps);
     flush_stats<STATS>(st, stats);
 }
 
@@ -884,7 +884,7 @@ __device__ __noinline__ void tail_exact(const rtk::WaveView& W, int l, uint32_t 
 #ifndef RT_TAIL_OCC
 #define RT_TAIL_OCC 3    // k_tail waves per SIMD (2: no spills but half the paths per launch; 3 measured faster)
 #endif
-template <bool STATS>
+template <bool STATS, bool PAIR = true>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TAIL_OCC, RT_TAIL_OCC))) void k_tail(rtk::WaveView W, int par, unsigned long long* stats)
 {
     __shared__ rtk::RayRec s_q[4][2][RT_TAIL_MAXP * rtk::RK_COUNT];  // per wave: closest list, occlusion list
@@ -981,7 +981,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TAIL_OCC
                 next = min(nq, next + __popcll(bidle));
             }
             if (act) {
-                const int res = l ? rtk::quad_visit<true, RT_TAIL_DESCEND>(S, q, stk, sub, ps)
+                const int res = l ? rtk::quad_visit<true, RT_TAIL_DESCEND, PAIR>(S, q, stk, sub, ps)
                                   : rtk::quad_visit<false, RT_TAIL_DESCEND>(S, q, stk, sub, ps);
                 if (res != 0) {
                     act = false;
@@ -1433,6 +1433,7 @@ int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounces, cons
     if (const char* e = getenv("RT_TRACE_FILLS")) trace_fills = std::max(0.25, atof(e));
     const int trace_blocks = (int)(dev_cus * trace_fills * RT_TRACE_OCC);
     const bool S = c->stats_enabled;
+    const bool SEQ = S && c->stats_seq;  // (counter renders with unpaired occlusion walks: rt_set_stats(ctx, 2))
     unsigned long long* stats = (unsigned long long*)b->stats.p;
     if (S) HIPCHK(c, hipMemsetAsync(b->stats.p, 0, b->stats.bytes, s));
     const char* iter_log = getenv("RT_ITER_LOG");  // per-iteration log of lane 0: counts (stats renders) / ms (timed)
@@ -1567,7 +1568,9 @@ int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounces, cons
             for (int k = 0; k < 3; k++)
                 if (!La.tev[k][La.it]) HIPCHK(c, hipEventCreate(&La.tev[k][La.it]));
         if (T) HIPCHK(c, hipEventRecord(La.tev[0][La.it], La.s));
-        if (S)
+        if (SEQ)
+            hipLaunchKernelGGL((k_trace<true, false>), dim3(trace_blocks_of(La)), dim3(threads), 0, La.s, W, par, stats);
+        else if (S)
             hipLaunchKernelGGL(k_trace<true>, dim3(trace_blocks_of(La)), dim3(threads), 0, La.s, W, par, stats);
         else
             hipLaunchKernelGGL(k_trace<false>, dim3(trace_blocks_of(La)), dim3(threads), 0, La.s, W, par, stats);
@@ -1618,7 +1621,9 @@ int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounces, cons
                 f[C_PARKA0 + (par ^ 1)] == 0) {  // (k_trace(i) released DONE[par ^ 1])
                 // few paths left and none waits: the tail kernel finishes them all
                 HIPCHK(c, hipMemsetAsync(La.cnt + C_TK_TAIL, 0, 4, La.s));
-                if (S)
+                if (SEQ)
+                    hipLaunchKernelGGL((k_tail<true, false>), dim3(tail_blocks), dim3(threads), 0, La.s, La.W, par, stats);
+                else if (S)
                     hipLaunchKernelGGL(k_tail<true>, dim3(tail_blocks), dim3(threads), 0, La.s, La.W, par, stats);
                 else
                     hipLaunchKernelGGL(k_tail<false>, dim3(tail_blocks), dim3(threads), 0, La.s, La.W, par, stats);

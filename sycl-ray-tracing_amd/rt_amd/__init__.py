@@ -328,8 +328,10 @@ class RenderKernel:
         """Tests only (rt_test_fail_device): later multi-device renders fail `device` (-1: off)."""
         check(self.L, self.L.rt_test_fail_device(self.ctx, int(device)), self.ctx, "rt_test_fail_device")
 
-    def set_stats(self, on: bool):
-        self.L.rt_set_stats(self.ctx, 1 if on else 0)
+    def set_stats(self, on):
+        """True / 1: counters of the next renders; 2: the same with unpaired occlusion walks
+        (the box tests a walk must make: same answers); False / 0: off."""
+        self.L.rt_set_stats(self.ctx, int(on) if not isinstance(on, bool) else (1 if on else 0))
 
     def stats(self) -> dict:
         """Counters of the last render (rt_set_stats(True) first), by name."""

@@ -39,7 +39,17 @@ def _worker(rank, world, port, q):
         f.render()
         full = f.gather(dst=0)
         if rank == 0:
-            q.put(full.numpy().copy())
+            # bench.py's N > 1 self-check: the gathered frame's rows against one device's
+            # render of the same rows (bitwise), and the same check on a frame whose rows
+            # were permuted (as a broken gather would leave them) must fail
+            import torch
+            sys.path.insert(0, os.path.dirname(here))
+            import bench
+            good = bench.multi_parity(full, rk, "cpu", torch, rows_every=5, first=2)
+            bad_frame = full.clone()
+            bad_frame[[2, 7]] = full[[7, 2]]
+            bad = bench.multi_parity(bad_frame, rk, "cpu", torch, rows_every=5, first=2)
+            q.put((full.numpy().copy(), good["ok"], good["bitwise_fraction"], bad["ok"], bad["bitwise_fraction"]))
     finally:
         dist.destroy_process_group()
 
@@ -53,9 +63,11 @@ def test_gloo_sharded_render_matches_golden(world):
     procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    full = q.get(timeout=300)
+    full, good_ok, good_frac, bad_ok, bad_frac = q.get(timeout=300)
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
     want = conftest.load_golden("render_cornell32_128.npz")["rgba"]
     np.testing.assert_array_equal(full.view(np.uint32), want.view(np.uint32))
+    assert good_ok and good_frac == 1.0
+    assert not bad_ok and bad_frac < 1.0

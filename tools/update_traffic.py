@@ -45,7 +45,9 @@ def main():
                   f"`bench.py --roofline-only --no-cpu-baseline --config {args.config}` (tools/profile_roofline.sh; "
                   "the <false> dispatches are the two 1-lane renders); FETCH KB x1024 x2 (gfx950 correction, "
                   "MI355X_MICROARCH.md), WRITE KB x1024, / dispatches" + (f"; build of commit {args.build}" if args.build else ""),
-        "round": 2,
+        "profile": f"{rel}/pmc_fetch.json",
+        "build": args.build or None,
+        "round": 4,
     }
     json.dump(t, open(p, "w"), indent=1)
     print(json.dumps(t[f"{args.config}_1lane"]))
