@@ -21,7 +21,7 @@ HIPFLAGS := -std=c++17 -O3 -fPIC --offload-arch=$(ARCH) -ffp-contract=off -fno-f
 
 HDRS := $(wildcard $(SRC)/*.h) include/rt_hip.h
 
-all: $(LIB)/librt_hip.so $(LIB)/librt_hostsim.so oracle/liboracle.so build/libm_check build/cdf_check
+all: $(LIB)/librt_hip.so $(LIB)/librt_hostsim.so oracle/liboracle.so build/libm_check build/cdf_check stamp
 
 $(OBJ)/%.host.o: $(SRC)/%.cpp $(HDRS)
 	@mkdir -p $(OBJ)
@@ -38,9 +38,13 @@ $(OBJ)/rt_render.o: $(SRC)/rt_render.hip $(HDRS)
 $(LIB)/librt_hip.so: $(OBJ)/rt_render.o $(OBJ)/rt_scene.host.o $(OBJ)/rt_imageio.host.o $(OBJ)/rt_capi_host.host.o
 	@mkdir -p $(LIB)
 	$(HIPCC) -shared --offload-arch=$(ARCH) -fPIC $^ -o $@
-	@# the commit the product library was built from (+ "-dirty" with uncommitted source changes): bench.py names it
-	@(git rev-parse --short HEAD 2>/dev/null || echo unknown) | tr -d '\n' > BUILD_COMMIT; \
-	  git diff --quiet HEAD -- $(SRC) include 2>/dev/null || printf -- "-dirty" >> BUILD_COMMIT
+
+# BUILD_COMMIT: "<commit>[-dirty] src=<hash of the kernel sources>", rewritten by every `make`
+# (the sources' hash names the build whatever was committed since; bench.py reports it)
+stamp: $(LIB)/librt_hip.so
+	@c=$$(git rev-parse --short HEAD 2>/dev/null || echo unknown); \
+	  git diff --quiet HEAD -- $(SRC) include 2>/dev/null || c="$$c-dirty"; \
+	  h=$$(cat $(SRC)/* include/*.h | sha256sum | cut -c1-12); echo "$$c src=$$h" > BUILD_COMMIT
 
 $(LIB)/librt_hostsim.so: $(OBJ)/rt_hostsim.o $(OBJ)/rt_scene.host.o $(OBJ)/rt_imageio.host.o $(OBJ)/rt_capi_host.host.o
 	@mkdir -p $(LIB)
@@ -64,7 +68,7 @@ ref:
 clean:
 	rm -rf $(OBJ) $(LIB) build/libm_check oracle/liboracle.so
 
-.PHONY: all ref clean
+.PHONY: all ref clean stamp
 
 # experiment builds: make variant V=name DEFS="-DRT_TAIL_OCC=2" -> lib/librt_hip_name.so (RT_HIP_LIB=...)
 variant: $(OBJ)/rt_scene.host.o $(OBJ)/rt_imageio.host.o $(OBJ)/rt_capi_host.host.o

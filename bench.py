@@ -242,8 +242,9 @@ def traffic_source(key):
     if e is None:
         return None
     now = build_commit()
+    src = lambda b: b.split("src=")[-1] if b and "src=" in b else None  # noqa: E731  (the kernel sources' hash)
     return {"profile": e.get("profile"), "build": e.get("build"), "running_build": now,
-            "same_build": bool(now and e.get("build") and now == e.get("build"))}
+            "same_build": bool(src(now) and src(now) == src(e.get("build")))}
 
 
 def load_traffic_class(key, cls):
