@@ -76,16 +76,6 @@ static int run_wave_host(rt_context* c, int w, int h, int spp, int bounces, cons
     if (mats) W.S.mats = mats;  // (rt_render_variants: a variant's table, same size as the bound one)
     W.cam = c->cam;
     W.src = src;
-    // the product's slot order (rt_render.hip run_wave): 8 x 8 tiles, one lane (RT_TILE_H: 0 / 2 / 4 / 8)
-    int tile_h = 8;
-    if (const char* e = getenv("RT_TILE_H")) tile_h = atoi(e);
-    if (!src.xy && (tile_h == 2 || tile_h == 4 || tile_h == 8)) {
-        W.src.th = tile_h;
-        W.src.tw = 64 / tile_h;
-        W.src.nl = 1;
-        W.src.l = 0;
-        W.src.rows = n / src.W;
-    }
     W.W = w;
     W.H = h;
     W.spp = spp;

@@ -51,9 +51,6 @@ namespace {
 #ifndef RT_STEP_OCC
 #define RT_STEP_OCC 3  // k_step waves per SIMD
 #endif
-#ifndef RT_TILE_H
-#define RT_TILE_H 8  // slot order: 8 x 8 pixel tiles (rt_wave.h PixSrc; RT_TILE_H env 0 = row order)
-#endif
 
 struct DevBuf {
     void* p = nullptr;
@@ -1447,12 +1444,7 @@ int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounces, cons
     // lanes: rows interleave (row j of the launch -> lane j % lanes); pixel lists split in runs
     int nl = b->lanes > 0 ? b->lanes : n <= RT_LANES4_MAX ? 4 : 3;
     const int rows = src.xy ? 0 : n / src.W;
-    // slot order: tiles of RT_TILE_H rows x 64 / RT_TILE_H columns (rt_wave.h PixSrc; 0 = row order)
-    int tile_h = RT_TILE_H;
-    if (const char* e = getenv("RT_TILE_H")) tile_h = atoi(e);
-    if (tile_h != 0 && tile_h != 1 && tile_h != 2 && tile_h != 4 && tile_h != 8) tile_h = RT_TILE_H;
-    if (tile_h == 1) tile_h = 0;
-    while (nl > 1 && (n < nl * 65536 || (!src.xy && rows < nl * (tile_h > 0 ? tile_h : 1)))) nl--;
+    while (nl > 1 && (n < nl * 65536 || (!src.xy && rows < nl))) nl--;
     WaveLane L[RT_MAX_LANES];
     int force_fb = 0;
     if (const char* e = getenv("RT_FORCE_FALLBACK")) force_fb = std::max(0, atoi(e));
@@ -1486,14 +1478,7 @@ int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounces, cons
         rtk::PixSrc ls = src;
         float4_* lfb = fb;
         int fb_rs = 1;
-        if (!src.xy && tile_h > 0) {  // tile order (rt_wave.h PixSrc): lanes interleave row blocks
-            ls.th = tile_h;
-            ls.tw = 64 / tile_h;
-            ls.nl = nl;
-            ls.l = l;
-            ls.rows = rows;
-            La.n = rtk::tile_lane_slots(src.W, rows, tile_h, nl, l);
-        } else if (nl == 1) {
+        if (nl == 1) {
             La.n = n;
         } else if (src.xy) {
             const int b0 = (int)((long)n * l / nl), b1 = (int)((long)n * (l + 1) / nl);

@@ -45,61 +45,23 @@ struct RayRec {  // 32 B queue entry
     float4_ d;  // xyz direction
 };
 
-// Pixel source of a launch: image rows y = off + j*stride of a shard (j = 0 .. rows-1),
-// or an explicit (x, y) list (ray_trace_pixel over a pixel set).
-//  * th == 0 (row order): slot i is shard row i / W, column i % W;
-//  * th > 0 (tile order): the shard's rows form blocks of th rows, block b belongs to
-//    lane b % nl, and a lane's slots run tile by tile (th rows x tw = 64 / th columns,
-//    the last tile of a row block narrower, the last block shorter), so the 64 paths
-//    of a wave — and the queries they emit, kept in slot order by the compactions —
-//    are a compact patch of the image instead of a 64-pixel strip of one row.
-// Answers do not depend on the slot order (pixels are independent); only locality does.
+// Pixel source of a launch: image rows y = off + j*stride (j = slot / W), or
+// an explicit (x, y) list (ray_trace_pixel over a pixel set).
 struct PixSrc {
     int W, off, stride;
     const int32_t* xy;
-    int th = 0, tw = 0;  // tile rows / columns (0: row order)
-    int nl = 1, l = 0;   // tile order: lanes interleaving the row blocks, and this lane
-    int rows = 0;        // tile order: rows of the shard
 };
-
-// Tile order: slot i of lane src.l -> column x and shard row srow.
-RT_HD void pix_tile(const PixSrc& src, int i, int& x, int& srow)
-{
-    const int W = src.W, th = src.th, tw = src.tw;
-    const int t = i / (th * W);  // the lane's row block (all but the shard's last block are full)
-    const int k = i - t * th * W;
-    const int blk = t * src.nl + src.l;
-    const int h = src.rows - blk * th < th ? src.rows - blk * th : th;
-    const int b = k / (tw * h);  // tile of the block (all but the last are full width)
-    const int wb = W - b * tw < tw ? W - b * tw : tw;
-    const int s = k - b * tw * h;
-    const int r = s / wb;
-    x = b * tw + (s - r * wb);
-    srow = blk * th + r;
-}
 
 RT_HD void pix_xy(const PixSrc& src, int i, int& x, int& y)
 {
     if (src.xy) {
         x = src.xy[2 * i];
         y = src.xy[2 * i + 1];
-    } else if (src.th > 0) {
-        int srow;
-        pix_tile(src, i, x, srow);
-        y = src.off + srow * src.stride;
     } else {
         const int j = i / src.W;
         x = i - j * src.W;
         y = src.off + j * src.stride;
     }
-}
-
-// Slots of lane l in tile order: W x the rows of its blocks (blocks b = l, l + nl, ...).
-inline int tile_lane_slots(int W, int rows, int th, int nl, int l)
-{
-    long n = 0;
-    for (int b = l; b * th < rows; b += nl) n += (rows - b * th < th ? rows - b * th : th);
-    return (int)(n * W);
 }
 
 struct WaveView {
@@ -403,13 +365,7 @@ RT_HD void set_view_consts(WaveView& W)
 // Framebuffer entry of slot p: slot rows map to every fb_rs-th framebuffer row.
 RT_HD size_t fb_at(const WaveView& W, int p)
 {
-    if (W.src.xy) return (size_t)p;
-    if (W.src.th > 0) {  // (tile order: fb is the shard's first row)
-        int x, srow;
-        pix_tile(W.src, p, x, srow);
-        return (size_t)srow * W.src.W + x;
-    }
-    if (W.fb_rs <= 1) return (size_t)p;
+    if (W.src.xy || W.fb_rs <= 1) return (size_t)p;
     const int j = p / W.src.W;
     return (size_t)j * W.fb_rs * W.src.W + (p - j * W.src.W);
 }
