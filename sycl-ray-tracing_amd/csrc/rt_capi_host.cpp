@@ -62,6 +62,7 @@ RtSceneView rt_host_view(const rt_context* c)
     v.n_tris = (int)(c->tris.size() / 9);
     v.chain_monotone = c->flat.chain_monotone ? 1 : 0;
     v.bvh4 = c->flat.bvh4.data();
+    v.bvh16 = c->flat.bvh16.data();
     v.bvh_tri4 = c->flat.bvh_tri4.data();
     v.parent = c->flat.parent.data();
     v.leaf_of = c->flat.leaf_of.data();

@@ -68,6 +68,12 @@ struct alignas(128) Bvh4Node {
     Bvh4Child ch[4];
 };
 static_assert(sizeof(Bvh4Node) == 128, "Bvh4Node must be 128 B");
+// 16-wide search BVH (rt_scene.cpp build_bvh16, walked by 16-lane rows: rt_row.h): node
+// i is records [16 i, 16 i + 16) of Bvh4Child, 512 B, one record per lane of a row. A
+// node holds two levels of the 4-wide tree: the leaf children of a 4-wide node and the
+// children of its inner children; an inner record's ref is a 16-wide node index. Same
+// boxes, same leaves (<= 4 triangles), so the same hits.
+#define RT_BVH16_W 16
 
 struct alignas(16) RtMat {
     float er, eg, eb, metalness;
@@ -96,6 +102,7 @@ struct RtSceneView {
     int32_t brute;  // 1: INTERSECT_SCENE is the brute-force loop (USE_BVH 0, render_kernel.cpp:453-483)
     // search BVH + octree back-links for the verification walk
     const Bvh4Node* bvh4;      // [0] = root
+    const Bvh4Child* bvh16;    // 16-wide form, RT_BVH16_W records per node, node 0 = root
     const float4_* bvh_tri4;   // 3 records per triangle in BVH leaf order: {a.xyz, k}, {e1, leaf record}, {e2}
     const int32_t* parent;     // octree record -> parent record (-1 for the root)
     const int32_t* leaf_of;    // leaf-order triangle k -> its octree leaf record

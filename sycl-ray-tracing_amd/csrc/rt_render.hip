@@ -35,6 +35,7 @@
 #include "rt_context.h"
 #include "rt_wave.h"
 #include "rt_quad.h"
+#include "rt_row.h"
 
 #define HIPCHK(ctx, expr)                                                                         \
     do {                                                                                          \
@@ -50,6 +51,12 @@ namespace {
 #define RT_LANES4_MAX 1572864  // auto lanes: 4 at most this many slots per launch, else 3
 #ifndef RT_STEP_OCC
 #define RT_STEP_OCC 3  // k_step waves per SIMD
+#endif
+#ifndef RT_ROW_BELOW
+#define RT_ROW_BELOW 0  // k_trace walks with rows (rt_row.h) below this many live paths per lane
+#endif
+#ifndef RT_TAIL_ROWS
+#define RT_TAIL_ROWS 0  // k_tail walks with rows (rt_row.h)
 #endif
 
 struct DevBuf {
@@ -151,7 +158,7 @@ struct Backend {
     int index = 0;    // position in the context's device list (0: the root)
     hipStream_t own = nullptr;  // device-side work not on a caller's stream (multi-device shards, pixel lists)
     DevBuf nodes, tri4, prim2k, mat_idx, mats, emissive, spheres, env, env_lum, cdf;
-    DevBuf bvh4, bvh_tri4, parent, leaf_of, cdf_row, cdf_coarse, cdf_fence, matk;
+    DevBuf bvh4, bvh16, bvh_tri4, parent, leaf_of, cdf_row, cdf_coarse, cdf_fence, matk;
     DevBuf stats;     // 2 x RT_STAT_COUNT u64: all kernels, then the tail kernel's share
     DevBuf iterq;     // stats renders: per-iteration {queries, live slots} (RT_ITER_LOG)
     DevBuf wave[RT_MAX_LANES];      // per lane: path state, pending records, results, queues, lists
@@ -423,6 +430,7 @@ __global__ __launch_bounds__(256) void k_tonemap(rtk::WaveView W)
 #define RT_LDS_CAP_ANY 16
 #define RT_REFILL 16
 #define RT_QSTACK 32            // quad walks (rt_quad.h): stack entries per quad (item + key, 64 quads per block)
+#define RT_RSTACK 64            // row walks (rt_row.h): stack entries per row (item + key, 16 rows per block)
 #define RT_TRACE_REFILL 4       // k_trace: idle quads of a wave that trigger a refill from its query stream
                                 // (r02, cfg2: 4 / 8 -> 726 / 723 vs 678 Msamples/s with static 16-query chunks)
 #ifndef RT_HEAVY_CALLS
@@ -665,12 +673,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_STEP_OCC
 }
 
 // k_trace's fast roles with per-quad refill (RT_TRACE_REFILL > 0): see k_trace.
-template <bool ANY, bool STATS, bool PAIR, class QSTK>
+// G = lanes per query: 4 (quads over the 4-wide BVH, rt_quad.h) or 16 (rows over the 16-wide
+// BVH, rt_row.h: half the trips per walk; sparse launches, where the longest walk sets the end).
+template <bool ANY, bool STATS, bool PAIR, int G, class QSTK>
 __device__ __forceinline__ void trace_stream(const rtk::WaveView& W, const RtSceneView& S, QSTK& stk, const int* s_pre,
                                              int first, int total, int wg, int wn, int32_t* fbn, rtk::RayRec* fbl,
                                              rtk::Stats* ps)
 {
-    const int lane = lane_id(), qd = lane >> 2, sub = lane & 3;
+    static_assert(G == 4 || G == 16, "quads or rows");
+    constexpr unsigned long long ALL_IDLE = G == 4 ? 0x1111111111111111ull : 0x0001000100010001ull;
+    constexpr int REFILL = G == 4 ? RT_TRACE_REFILL : 1;  // idle groups that trigger a refill
+    const int lane = lane_id(), qd = lane / G, sub = lane & (G - 1);
     int cursor = 0;                     // the wave's next stream position (uniform)
     bool exhausted = wg * 16 >= total;  // (uniform)
     bool active = false;
@@ -678,9 +691,9 @@ __device__ __forceinline__ void trace_stream(const rtk::WaveView& W, const RtSce
     rtk::QState q;  // (its ray is the query's: a fallback record is rebuilt from q.o, q.d and target)
     for (;;) {
         const unsigned long long bidle = __ballot(!active && sub == 0);
-        if (!exhausted && (__popcll(bidle) >= RT_TRACE_REFILL || bidle == 0x1111111111111111ull)) {
+        if (!exhausted && (__popcll(bidle) >= REFILL || bidle == ALL_IDLE)) {
             if (!active) {
-                const int j = cursor + __popcll(bidle & ((1ull << (qd * 4)) - 1ull));  // this quad's stream position
+                const int j = cursor + __popcll(bidle & ((1ull << (qd * G)) - 1ull));  // this group's stream position
                 const int idx = (wg + (j >> 4) * wn) * 16 + (j & 15);
                 if (idx < total) {
                     int kind;
@@ -713,10 +726,14 @@ __device__ __forceinline__ void trace_stream(const rtk::WaveView& W, const RtSce
         }
         if (STATS) {  // SIMT slots of this trip: 16 quads, the active ones used
             if (active && sub == 0) ps->c[exhausted ? RT_STAT_DRAIN_VISITS : RT_STAT_QUAD_VISITS]++;
-            if (lane == 0) ps->c[exhausted ? RT_STAT_DRAIN_SLOTS : RT_STAT_WAVE_SLOTS] += 16;
+            if (lane == 0) ps->c[exhausted ? RT_STAT_DRAIN_SLOTS : RT_STAT_WAVE_SLOTS] += 64 / G;
         }
         if (active) {
-            int res = rtk::quad_visit<ANY, RT_VISIT_DESCEND, PAIR>(S, q, stk, sub, ps);
+            int res;
+            if constexpr (G == 4)
+                res = rtk::quad_visit<ANY, RT_VISIT_DESCEND, PAIR>(S, q, stk, sub, ps);
+            else
+                res = rtk::row_visit<ANY, RT_VISIT_DESCEND>(S, q, stk, sub, ps);
             q.calls++;
             if (res != 0) {
                 active = false;
@@ -731,7 +748,9 @@ __device__ __forceinline__ void trace_stream(const rtk::WaveView& W, const RtSce
                 }
                 float t = 0.0f;
                 int k = 0;
-                if (res > 0 && !ANY && !rtk::quad_closest_answer(S, q, sub, t, k, ps)) res = -1;
+                // (rows: each quad of the row verifies alike; one counts)
+                if (res > 0 && !ANY && !rtk::quad_closest_answer(S, q, sub & 3, t, k, G == 4 || sub == 0 ? ps : nullptr))
+                    res = -1;
                 if (sub == 0) {
                     if (res > 0) {
                         if (ANY)
@@ -749,7 +768,7 @@ __device__ __forceinline__ void trace_stream(const rtk::WaveView& W, const RtSce
     }
 }
 
-template <bool STATS, bool PAIR = true>
+template <bool STATS, bool PAIR = true, int G = 4>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_OCC, 8))) void k_trace(rtk::WaveView W, int par, unsigned long long* stats)
 {
     __shared__ uint32_t s_lds[RT_LDS_WORDS * 256];
@@ -779,8 +798,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_OC
     const int b = (int)blockIdx.x;
 
     const RtSceneView S = W.S;
-    // fast roles: a quad of lanes per query (rt_quad.h), 16 queries per wave
-    rtk::QuadStack<RT_QSTACK, 64> stk{s_lds + (threadIdx.x >> 2), (float*)s_lds + RT_QSTACK * 64 + (threadIdx.x >> 2)};
+    // fast roles: a quad of lanes per query (rt_quad.h), or a row of 16 (rt_row.h)
     // queue segments in stream order (seg_id: each role's heavy class first): prefix table in LDS
     shard_prefix(cnt, RT_NSEG, [&](int j) { return seg_counter(par, j); }, s_pre);
     // without occlusion walks (analytic spheres) every kind is a closest-hit query
@@ -802,10 +820,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_OC
     // each quad walks one, one trip per loop (rt_quad.h quad_visit), and as soon as
     // RT_TRACE_REFILL quads are idle they all take the next queries, so a long walk holds
     // up its own quad, not the wave's next 15 queries.
-    if (closest)
-        trace_stream<false, STATS, PAIR>(W, S, stk, s_pre, c0, total, wg, wn, fbn, fbl, ps);
-    else
-        trace_stream<true, STATS, PAIR>(W, S, stk, s_pre, a0, total, wg, wn, fbn, fbl, ps);
+    if constexpr (G == 4) {
+        rtk::QuadStack<RT_QSTACK, 64> stk{s_lds + (threadIdx.x >> 2), (float*)s_lds + RT_QSTACK * 64 + (threadIdx.x >> 2)};
+        if (closest)
+            trace_stream<false, STATS, PAIR, 4>(W, S, stk, s_pre, c0, total, wg, wn, fbn, fbl, ps);
+        else
+            trace_stream<true, STATS, PAIR, 4>(W, S, stk, s_pre, a0, total, wg, wn, fbn, fbl, ps);
+    } else {
+        static_assert(2 * RT_RSTACK * 16 <= RT_LDS_WORDS * 256, "row stacks fit k_trace's LDS");
+        rtk::QuadStack<RT_RSTACK, 16> stk{s_lds + (threadIdx.x >> 4), (float*)s_lds + RT_RSTACK * 16 + (threadIdx.x >> 4)};
+        if (closest)
+            trace_stream<false, STATS, PAIR, 16>(W, S, stk, s_pre, c0, total, wg, wn, fbn, fbl, ps);
+        else
+            trace_stream<true, STATS, PAIR, 16>(W, S, stk, s_pre, a0, total, wg, wn, fbn, fbl, ps);
+    }
     flush_stats<STATS>(st, stats);
 }
 
@@ -884,7 +912,7 @@ __device__ __noinline__ void tail_exact(const rtk::WaveView& W, int l, uint32_t 
 #ifndef RT_TAIL_OCC
 #define RT_TAIL_OCC 3    // k_tail waves per SIMD (2: no spills but half the paths per launch; 3 measured faster)
 #endif
-template <bool STATS, bool PAIR = true>
+template <bool STATS, bool PAIR = true, int G = 4>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TAIL_OCC, RT_TAIL_OCC))) void k_tail(rtk::WaveView W, int par, unsigned long long* stats)
 {
     __shared__ rtk::RayRec s_q[4][2][RT_TAIL_MAXP * rtk::RK_COUNT];  // per wave: closest list, occlusion list
@@ -900,10 +928,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TAIL_OCC
     if (STATS)
         for (int i = 0; i < RT_STAT_COUNT; i++) st.c[i] = 0;
     rtk::Stats* ps = STATS ? &st : nullptr;
-    const int wv = (int)(threadIdx.x >> 6), lane = lane_id(), sub = lane & 3, qd = (int)(threadIdx.x >> 2);
-    rtk::QuadStack<RT_QSTACK, 64> stk{s_stk + qd, (float*)s_stk + RT_QSTACK * 64 + qd};
+    // G lanes per query: quads (4-wide BVH) or rows (16-wide BVH, rt_row.h), each with its LDS stack
+    static_assert(G == 4 || G == 16, "quads or rows");
+    constexpr int SCAP = G == 4 ? RT_QSTACK : RT_RSTACK, GPB = 256 / G;
+    static_assert(2 * SCAP * GPB <= 2 * RT_QSTACK * 64, "group stacks fit k_tail's LDS");
+    const int wv = (int)(threadIdx.x >> 6), lane = lane_id(), sub = lane & (G - 1), qd = (int)(threadIdx.x / G);
+    using STK = rtk::QuadStack<SCAP, GPB>;
+    STK stk{s_stk + qd, (float*)s_stk + SCAP * GPB + qd};
     const size_t gl = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    rtk::SpillStack<rtk::QuadStack<RT_QSTACK, 64>> xs{stk, W.spill_r + gl * RT_STACK_CAP, W.spill_k + gl * RT_STACK_CAP};
+    rtk::SpillStack<STK> xs{stk, W.spill_r + gl * RT_STACK_CAP, W.spill_k + gl * RT_STACK_CAP};
     const int P = W.tail_paths;
     const int last_kind = W.any_rays ? rtk::RK_CAM : rtk::RK_BENV;
     int my = -1;
@@ -959,7 +992,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TAIL_OCC
             bool exact = false;
             const unsigned long long bidle = __ballot(!act && sub == 0);
             if (next < nq) {
-                const int qi = next + __popcll(bidle & ((1ull << (lane & ~3)) - 1ull));  // this quad's query
+                const int qi = next + __popcll(bidle & ((1ull << (lane & ~(G - 1))) - 1ull));  // this group's query
                 if (!act && qi < nq) {
                     l = qi < nl[0] ? 0 : 1;
                     const rtk::RayRec r = s_q[wv][l][l ? qi - nl[0] : qi];
@@ -981,13 +1014,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TAIL_OCC
                 next = min(nq, next + __popcll(bidle));
             }
             if (act) {
-                const int res = l ? rtk::quad_visit<true, RT_TAIL_DESCEND, PAIR>(S, q, stk, sub, ps)
-                                  : rtk::quad_visit<false, RT_TAIL_DESCEND>(S, q, stk, sub, ps);
+                int res;
+                if constexpr (G == 4)
+                    res = l ? rtk::quad_visit<true, RT_TAIL_DESCEND, PAIR>(S, q, stk, sub, ps)
+                            : rtk::quad_visit<false, RT_TAIL_DESCEND>(S, q, stk, sub, ps);
+                else
+                    res = l ? rtk::row_visit<true, RT_TAIL_DESCEND>(S, q, stk, sub, ps)
+                            : rtk::row_visit<false, RT_TAIL_DESCEND>(S, q, stk, sub, ps);
                 if (res != 0) {
                     act = false;
                     float t = 0.0f;
                     int k = 0;
-                    const bool ok = res > 0 && (l == 1 || rtk::quad_closest_answer(S, q, sub, t, k, ps));
+                    const bool ok = res > 0 && (l == 1 || rtk::quad_closest_answer(S, q, sub & 3, t, k,
+                                                                                    G == 4 || sub == 0 ? ps : nullptr));
                     if (ok && sub == 0) {
                         if (l == 0)
                             rtk::finish_closest(W, target, q.o, q.d, t, k);
@@ -1095,6 +1134,37 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
         float t = -1.0f;
         int k = -1;
         const bool ok = res > 0 && (ANY || rtk::quad_closest_answer(S, qs, sub, t, k, nullptr));
+        if (sub == 0) {
+            if (ANY) {
+                out_t[i] = ok ? (float)(qs.h.k == 1 ? 1 : 0) : -2.0f;
+                out_k[i] = 0;
+            } else {
+                out_t[i] = ok ? t : -2.0f;
+                out_k[i] = ok ? k : -2;
+            }
+        }
+    }
+}
+
+// The same through the row walks (rt_row.h row_visit over the 16-wide BVH): 16 lanes per query.
+template <bool ANY>
+__global__ __launch_bounds__(256) void k_query_row(RtSceneView S, const float4_* __restrict__ rays,
+                                                   float* __restrict__ out_t, int* __restrict__ out_k, int n)
+{
+    __shared__ uint32_t s_lds[2 * RT_RSTACK * 16];
+    const int r = (int)(threadIdx.x >> 4), sub = (int)(threadIdx.x & 15);
+    rtk::QuadStack<RT_RSTACK, 16> stk{s_lds + r, (float*)s_lds + RT_RSTACK * 16 + r};
+    const int stride = (int)(gridDim.x * blockDim.x) >> 4;
+    for (int i = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 4); i < n; i += stride) {
+        rtk::QState qs;
+        int res = 1;
+        if (rtk::qstate_begin<ANY>(qs, rtk::v3of(rays[2 * i]), rtk::v3of(rays[2 * i + 1]), sub, nullptr))
+            do {
+                res = rtk::row_visit<ANY, RT_VISIT_DESCEND>(S, qs, stk, sub, nullptr);
+            } while (res == 0);
+        float t = -1.0f;
+        int k = -1;
+        const bool ok = res > 0 && (ANY || rtk::quad_closest_answer(S, qs, sub & 3, t, k, nullptr));
         if (sub == 0) {
             if (ANY) {
                 out_t[i] = ok ? (float)(qs.h.k == 1 ? 1 : 0) : -2.0f;
@@ -1231,7 +1301,7 @@ void destroy_one(Backend* b)
     (void)hipSetDevice(b->device);
     (void)hipDeviceSynchronize();
     DevBuf* all[] = {&b->nodes, &b->tri4, &b->prim2k, &b->mat_idx, &b->mats, &b->emissive, &b->spheres, &b->env,
-                     &b->env_lum, &b->cdf, &b->bvh4, &b->bvh_tri4, &b->parent, &b->leaf_of, &b->cdf_row, &b->cdf_coarse,
+                     &b->env_lum, &b->cdf, &b->bvh4, &b->bvh16, &b->bvh_tri4, &b->parent, &b->leaf_of, &b->cdf_row, &b->cdf_coarse,
                      &b->cdf_fence, &b->matk, &b->stats, &b->xy, &b->fb, &b->iterq};
     for (DevBuf* d : all)
         if (d->p) (void)hipFree(d->p);
@@ -1279,7 +1349,8 @@ int upload_one(rt_context* c, Backend* b, const std::vector<int32_t>& matk, bool
         (r = upload(c, b->mats, c->mats)) || (r = upload(c, b->emissive, c->emissive)) ||
         (r = upload(c, b->spheres, c->spheres)) || (r = upload(c, b->env, c->env)) ||
         (r = upload(c, b->env_lum, c->env_lum)) || (r = upload(c, b->cdf, c->cdf)) ||
-        (r = upload(c, b->bvh4, c->flat.bvh4)) || (r = upload(c, b->bvh_tri4, c->flat.bvh_tri4)) ||
+        (r = upload(c, b->bvh4, c->flat.bvh4)) || (r = upload(c, b->bvh16, c->flat.bvh16)) ||
+        (r = upload(c, b->bvh_tri4, c->flat.bvh_tri4)) ||
         (r = upload(c, b->parent, c->flat.parent)) || (r = upload(c, b->leaf_of, c->flat.leaf_of)) ||
         (r = upload(c, b->cdf_row, c->cdf_row)) || (r = upload(c, b->cdf_coarse, c->cdf_coarse)) ||
         (r = upload(c, b->cdf_fence, c->cdf_fence)) || (r = upload(c, b->matk, matk)) ||
@@ -1313,6 +1384,7 @@ int upload_one(rt_context* c, Backend* b, const std::vector<int32_t>& matk, bool
     v.chain_monotone = c->flat.chain_monotone ? 1 : 0;
     v.brute = c->brute ? 1 : 0;
     v.bvh4 = (const Bvh4Node*)b->bvh4.p;
+    v.bvh16 = (const Bvh4Child*)b->bvh16.p;
     v.bvh_tri4 = (const float4_*)b->bvh_tri4.p;
     v.parent = (const int32_t*)b->parent.p;
     v.leaf_of = (const int32_t*)b->leaf_of.p;
@@ -1458,6 +1530,12 @@ int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounces, cons
     // 887-890 Msamples/s, cfg4 8-way shard (slowest rank) 401 / - / 390 / 405 ms
     int tail_p = 2;
     if (const char* e = getenv("RT_TAIL_PATHS")) tail_p = std::min(RT_TAIL_MAXP, std::max(0, atoi(e)));
+    // row walks (rt_row.h, 16 lanes per query over the 16-wide BVH) where walks are latency-bound:
+    // k_trace launches of lanes with fewer than row_below live paths, and the tail kernel (tail_rows)
+    long row_below = RT_ROW_BELOW;
+    if (const char* e = getenv("RT_ROW_BELOW")) row_below = atol(e);
+    int tail_rows = RT_TAIL_ROWS;
+    if (const char* e = getenv("RT_TAIL_ROWS")) tail_rows = atoi(e) != 0;
     const int tail_blocks = dev_cus * RT_TAIL_OCC;  // one grid-fill of k_tail
     // a lane enters the tail kernel at 2x one grid-fill's pool (the waves refill from the live
     // list): with 2 paths per wave, RT_TAIL_ENTER = 1.4 / 1.75 / 2.2 / 2.8 -> cfg2 888-897 /
@@ -1568,12 +1646,15 @@ int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounces, cons
             for (int k = 0; k < 3; k++)
                 if (!La.tev[k][La.it]) HIPCHK(c, hipEventCreate(&La.tev[k][La.it]));
         if (T) HIPCHK(c, hipEventRecord(La.tev[0][La.it], La.s));
+        // sparse launches (few live paths: the launch ends with its longest walk) walk with rows
+        const bool rows = La.live < row_below;
+        const dim3 g(trace_blocks_of(La));
         if (SEQ)
-            hipLaunchKernelGGL((k_trace<true, false>), dim3(trace_blocks_of(La)), dim3(threads), 0, La.s, W, par, stats);
+            hipLaunchKernelGGL((rows ? k_trace<true, false, 16> : k_trace<true, false, 4>), g, dim3(threads), 0, La.s, W, par, stats);
         else if (S)
-            hipLaunchKernelGGL(k_trace<true>, dim3(trace_blocks_of(La)), dim3(threads), 0, La.s, W, par, stats);
+            hipLaunchKernelGGL((rows ? k_trace<true, true, 16> : k_trace<true, true, 4>), g, dim3(threads), 0, La.s, W, par, stats);
         else
-            hipLaunchKernelGGL(k_trace<false>, dim3(trace_blocks_of(La)), dim3(threads), 0, La.s, W, par, stats);
+            hipLaunchKernelGGL((rows ? k_trace<false, true, 16> : k_trace<false, true, 4>), g, dim3(threads), 0, La.s, W, par, stats);
         if (T) HIPCHK(c, hipEventRecord(La.tev[1][La.it], La.s));
         HIPCHK(c, hipGetLastError());
         return RT_OK;
@@ -1621,12 +1702,13 @@ int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounces, cons
                 f[C_PARKA0 + (par ^ 1)] == 0) {  // (k_trace(i) released DONE[par ^ 1])
                 // few paths left and none waits: the tail kernel finishes them all
                 HIPCHK(c, hipMemsetAsync(La.cnt + C_TK_TAIL, 0, 4, La.s));
+                const dim3 g(tail_blocks);
                 if (SEQ)
-                    hipLaunchKernelGGL((k_tail<true, false>), dim3(tail_blocks), dim3(threads), 0, La.s, La.W, par, stats);
+                    hipLaunchKernelGGL((tail_rows ? k_tail<true, false, 16> : k_tail<true, false, 4>), g, dim3(threads), 0, La.s, La.W, par, stats);
                 else if (S)
-                    hipLaunchKernelGGL(k_tail<true>, dim3(tail_blocks), dim3(threads), 0, La.s, La.W, par, stats);
+                    hipLaunchKernelGGL((tail_rows ? k_tail<true, true, 16> : k_tail<true, true, 4>), g, dim3(threads), 0, La.s, La.W, par, stats);
                 else
-                    hipLaunchKernelGGL(k_tail<false>, dim3(tail_blocks), dim3(threads), 0, La.s, La.W, par, stats);
+                    hipLaunchKernelGGL((tail_rows ? k_tail<false, true, 16> : k_tail<false, true, 4>), g, dim3(threads), 0, La.s, La.W, par, stats);
                 if (b->timing && La.it < RT_MAX_TIMED_ITERS) HIPCHK(c, hipEventRecord(La.tev[2][La.it], La.s));
                 HIPCHK(c, hipGetLastError());
                 La.tail_iter = La.it;
@@ -2068,6 +2150,7 @@ extern "C" int rt_device_queries(rt_context* c, int mode, const float* rays, int
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, b->device);
     const int threads = 256, blocks = std::min((n + threads - 1) / threads, cus * 8);
     const int qblocks = std::min((4 * n + threads - 1) / threads, cus * 16);
+    const int rblocks = std::min((16 * n + threads - 1) / threads, cus * 16);
     float4_* d_rays = nullptr;
     float* d_t = nullptr;
     int* d_k = nullptr;
@@ -2089,7 +2172,9 @@ extern "C" int rt_device_queries(rt_context* c, int mode, const float* rays, int
             case 4: hipLaunchKernelGGL((k_query_quad<false, 1>), dim3(qblocks), dim3(threads), 0, 0, b->view, d_rays, d_t, d_k, n); break;
             case 5: hipLaunchKernelGGL((k_query_quad<true, 1>), dim3(qblocks), dim3(threads), 0, 0, b->view, d_rays, d_t, d_k, n); break;
             case 6: hipLaunchKernelGGL((k_query_quad<false, 8>), dim3(qblocks), dim3(threads), 0, 0, b->view, d_rays, d_t, d_k, n); break;
-            default: hipLaunchKernelGGL((k_query_quad<true, 8>), dim3(qblocks), dim3(threads), 0, 0, b->view, d_rays, d_t, d_k, n); break;
+            case 7: hipLaunchKernelGGL((k_query_quad<true, 8>), dim3(qblocks), dim3(threads), 0, 0, b->view, d_rays, d_t, d_k, n); break;
+            case 8: hipLaunchKernelGGL((k_query_row<false>), dim3(rblocks), dim3(threads), 0, 0, b->view, d_rays, d_t, d_k, n); break;
+            default: hipLaunchKernelGGL((k_query_row<true>), dim3(rblocks), dim3(threads), 0, 0, b->view, d_rays, d_t, d_k, n); break;
         }
     };
     launch();  // warm-up

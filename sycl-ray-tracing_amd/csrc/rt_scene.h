@@ -75,6 +75,8 @@ struct FlatBvh {
     std::vector<BvhNode> bvh;    // binary SAH build
     std::vector<Bvh4Node> bvh4;  // collapsed 4-wide form the device walks (first bvh4_ntop: breadth-first top)
     int bvh4_ntop = 0;
+    // 16-wide form (two bvh4 levels per node, rt_device.h Bvh16): 16 child records per node
+    std::vector<Bvh4Child> bvh16;
     std::vector<float4_> bvh_tri4;
 };
 void flatten_octree(const Octree& t, const float* tris, int ntris, FlatBvh& out);
