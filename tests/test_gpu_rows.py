@@ -56,6 +56,7 @@ def test_gpu_row_walks_match_quad_walks_and_octree():
     o = np.tile(cam.view_matrix[:3, 3][None], (4096, 1)).astype(np.float32)
     d = rng.normal(size=(4096, 3)).astype(np.float32) * np.float32(0.15) + np.float32([0, -0.45, -1.0])
     sets["camera"] = _rays8(o, (d / np.linalg.norm(d, axis=1, keepdims=True)).astype(np.float32))
+    seen_unoccluded = False
     for name, rays in sets.items():
         tq, kq = _queries(rk, 4, rays)   # closest, quad walk
         tr, kr = _queries(rk, 8, rays)   # closest, row walk
@@ -64,9 +65,11 @@ def test_gpu_row_walks_match_quad_walks_and_octree():
         aq, _ = _queries(rk, 5, rays)    # occlusion, quad walk
         ar, _ = _queries(rk, 9, rays)    # occlusion, row walk
         np.testing.assert_array_equal(ar.view(np.uint32), aq.view(np.uint32), err_msg=f"{name}: occlusion")
-        assert (tr > 0).any() and (ar == 1.0).any() and (ar == 0.0).any(), name
+        assert (tr > 0).any() and (ar == 1.0).any(), name
+        seen_unoccluded = seen_unoccluded or bool((ar == 0.0).any())
         # the settled closest answers against the exact octree walk (BVH::intersect)
         ok = tr != -2.0
         ex = rk.intersect(rays[ok][:, [0, 1, 2, 4, 5, 6]])
         np.testing.assert_array_equal(np.where(ex[:, 0] == 1, ex[:, 2].view(np.float32), -1.0).astype(np.float32)
                                       .view(np.uint32), tr[ok].view(np.uint32), err_msg=f"{name}: vs octree")
+    assert seen_unoccluded
