@@ -56,7 +56,7 @@ namespace {
 #define RT_ROW_BELOW 0  // k_trace walks with rows (rt_row.h) below this many live paths per lane
 #endif
 #ifndef RT_TAIL_ROWS
-#define RT_TAIL_ROWS 0  // k_tail walks with rows (rt_row.h)
+#define RT_TAIL_ROWS 1  // k_tail walks with rows (rt_row.h)
 #endif
 
 struct DevBuf {
@@ -1528,14 +1528,20 @@ int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounces, cons
     // fewer paths per wave move each chain faster. With the entry held at the same live count
     // (r03, P x RT_TAIL_ENTER = 3.5): P = 5 / 3 / 2 / 1 -> cfg2 886-893 / 892-896 / 897-901 /
     // 887-890 Msamples/s, cfg4 8-way shard (slowest rank) 401 / - / 390 / 405 ms
-    int tail_p = 2;
-    if (const char* e = getenv("RT_TAIL_PATHS")) tail_p = std::min(RT_TAIL_MAXP, std::max(0, atoi(e)));
     // row walks (rt_row.h, 16 lanes per query over the 16-wide BVH) where walks are latency-bound:
-    // k_trace launches of lanes with fewer than row_below live paths, and the tail kernel (tail_rows)
+    // the tail kernel (tail_rows, on: its rounds wait for their slowest walk), and k_trace launches
+    // of lanes with fewer than row_below live paths (off: a sparse launch still has more queries
+    // than rows, and a row walk's throughput is lower). cfg4 8-way shard, one MI355X
+    // (profiles/r04c_row_probe.json, r04d_tail_probe.json): quads 380-382 ms; tail rows 367-370;
+    // k_trace rows below 32 K / 131 K paths 415 / 420-428 ms.
     long row_below = RT_ROW_BELOW;
     if (const char* e = getenv("RT_ROW_BELOW")) row_below = atol(e);
     int tail_rows = RT_TAIL_ROWS;
     if (const char* e = getenv("RT_TAIL_ROWS")) tail_rows = atoi(e) != 0;
+    // (rows: one path per wave, its ~4 queries on the wave's 4 rows: shard 367 ms vs 2 / 3 paths
+    // 373-378 / 373-375 at the same entry live count)
+    int tail_p = tail_rows ? 1 : 2;
+    if (const char* e = getenv("RT_TAIL_PATHS")) tail_p = std::min(RT_TAIL_MAXP, std::max(0, atoi(e)));
     const int tail_blocks = dev_cus * RT_TAIL_OCC;  // one grid-fill of k_tail
     // a lane enters the tail kernel at 2x one grid-fill's pool (the waves refill from the live
     // list): with 2 paths per wave, RT_TAIL_ENTER = 1.4 / 1.75 / 2.2 / 2.8 -> cfg2 888-897 /

@@ -265,7 +265,8 @@ def test_gpu_slab_division_exact():
 
 def test_gpu_schedules_bit_identical(monkeypatch):
     """The frame does not depend on the schedule: 1-4 wavefront lanes, the
-    tail kernel on or off (1-8 paths per wave, entered at once or late), row
+    tail kernel on or off (1-8 paths per wave, entered at once or late), quad or
+    row walks (rt_row.h) in the tail kernel and in k_trace, row
     shards split across lanes (framebuffer row pitch), k_trace's heavy class
     (off, every walk heavy, the default) and the camera ray traced ahead or not
     all give the same bits as one lane without the tail kernel."""
@@ -275,7 +276,9 @@ def test_gpu_schedules_bit_identical(monkeypatch):
     sky = scenes.make_sky("L")
     W, H, spp, nb = 640, 480, 2, 8
 
-    def render(lanes, tail, off=0, stride=1, heavy=6, enter=2.0, spec_cam=1):
+    def render(lanes, tail, off=0, stride=1, heavy=6, enter=2.0, spec_cam=1, rows=1, row_below=0):
+        monkeypatch.setenv("RT_TAIL_ROWS", str(rows))
+        monkeypatch.setenv("RT_ROW_BELOW", str(row_below))
         monkeypatch.setenv("RT_LANES", str(lanes))
         monkeypatch.setenv("RT_TAIL_PATHS", str(tail))
         monkeypatch.setenv("RT_HEAVY", str(heavy))
@@ -313,6 +316,11 @@ def test_gpu_schedules_bit_identical(monkeypatch):
     for lanes, tail in ((1, 0), (3, 2)):
         got = render(lanes, tail, spec_cam=0)
         np.testing.assert_array_equal(got.view(np.uint32), base.view(np.uint32), err_msg=f"spec_cam=0 lanes={lanes}")
+    # the walks by quads or by rows (rt_row.h) in the tail kernel, and rows in every k_trace launch
+    for rows, row_below, tail, enter in ((0, 0, 2, 2.0), (1, 0, 1, 1000.0), (1, 1 << 30, 1, 2.0), (0, 1 << 30, 4, 2.0)):
+        got = render(3, tail, enter=enter, rows=rows, row_below=row_below)
+        np.testing.assert_array_equal(got.view(np.uint32), base.view(np.uint32),
+                                      err_msg=f"rows={rows} row_below={row_below} tail={tail}")
 
 
 @pytest.mark.gpu
