@@ -55,9 +55,6 @@ namespace {
 #ifndef RT_ROW_BELOW
 #define RT_ROW_BELOW 0  // k_trace walks with rows (rt_row.h) below this many live paths per lane
 #endif
-#ifndef RT_HEAVY_ROWS
-#define RT_HEAVY_ROWS 0  // k_trace walks its heavy class (predicted-long walks) with rows
-#endif
 #ifndef RT_TAIL_ROWS
 #define RT_TAIL_ROWS 1  // k_tail walks with rows (rt_row.h)
 #endif
@@ -741,8 +738,7 @@ __device__ __forceinline__ void trace_stream(const rtk::WaveView& W, const RtSce
             if (res != 0) {
                 active = false;
                 // a long walk: the path's next rays go to the heavy class (head of the next streams)
-                // (a row call covers two 4-wide levels: half the calls of a quad walk)
-                if (W.r_heavy && sub == 0 && (G == 4 ? q.calls : 2 * q.calls) >= W.heavy_calls) W.r_heavy[target >> 3] = 1;
+                if (W.r_heavy && sub == 0 && q.calls >= W.heavy_calls) W.r_heavy[target >> 3] = 1;
                 if (STATS && W.iterq && sub == 0 && W.iter < RT_MAX_TIMED_ITERS) {
                     // (RT_ITER_LOG: the launch's longest walk in quad_visit calls per role, and
                     // how many walks took more than 8)
@@ -772,7 +768,6 @@ __device__ __forceinline__ void trace_stream(const rtk::WaveView& W, const RtSce
     }
 }
 
-// G: 4 quads, 16 rows, 0 the heavy class by rows and the rest by quads
 template <bool STATS, bool PAIR = true, int G = 4>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_OCC, 8))) void k_trace(rtk::WaveView W, int par, unsigned long long* stats)
 {
@@ -811,59 +806,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_OC
     const int nc = (W.any_rays ? a0 : s_pre[RT_SEG_END]) - c0;
     const int na = W.any_rays ? s_pre[RT_SEG_END] - a0 : 0;
     if (STATS && W.iterq && b == 0 && threadIdx.x == 0 && W.iter < RT_MAX_TIMED_ITERS) W.iterq[2 * W.iter] = nc + na;
-    // The wave's queries are a stream (its 16-query chunks base = wg*16 + c*wn*16 in turn):
-    // each group walks one, one trip per loop (quad_visit / row_visit), and as soon as
-    // enough groups are idle they take the next queries, so a long walk holds up its own
-    // group, not the wave's next 15 queries.
-    if constexpr (G == 0) {
-        // heavy rows: each role's heavy class (the rays of paths whose last walk was long,
-        // seg_id) walked by rows, the rest by quads: four roles, blocks split by the lanes
-        // their queries take (16 per heavy query, 4 per other)
-        int lo[4], n[4];
-        lo[0] = c0, n[0] = s_pre[RT_SEG_CH] - c0;
-        lo[1] = s_pre[RT_SEG_CH], n[1] = c0 + nc - lo[1];
-        lo[2] = a0, n[2] = W.any_rays ? s_pre[RT_SEG_A] - a0 : 0;
-        lo[3] = W.any_rays ? s_pre[RT_SEG_A] : a0, n[3] = na - n[2];
-        long w[4] = {16l * n[0], 4l * n[1], 16l * n[2], 4l * n[3]};
-        const int nb = (int)gridDim.x;
-        int cntb[4], used = 0, big = 0;
-        long wsum = 0;
-        for (int r = 0; r < 4; r++) wsum += w[r];
-        for (int r = 0; r < 4; r++) {
-            cntb[r] = w[r] > 0 ? 1 : 0;
-            used += cntb[r];
-        }
-        const int spare = nb - used;
-        for (int r = 0; r < 4; r++) {
-            if (w[r] > 0 && wsum > 0) cntb[r] += (int)((long)spare * w[r] / wsum);
-            if (w[r] > w[big]) big = r;
-        }
-        int tot = 0;
-        for (int r = 0; r < 4; r++) tot += cntb[r];
-        cntb[big] += nb - tot;  // (rounding leftovers)
-        int r = 0, start = 0;
-        while (r < 3 && b >= start + cntb[r]) start += cntb[r++];
-        const int rb = b - start, rnb = cntb[r];
-        const int wg = rb * (int)(blockDim.x >> 6) + (int)(threadIdx.x >> 6), wn = rnb * (int)(blockDim.x >> 6);
-        const bool closest = r < 2;
-        int32_t* fbn = cnt + (closest ? C_FBC0 : C_FBA0) + par;  // walked exactly by k_step(i)
-        rtk::RayRec* fbl = closest ? W.fb_c[par] : W.fb_a[par];
-        if (r == 0 || r == 2) {
-            rtk::QuadStack<RT_RSTACK, 16> stk{s_lds + (threadIdx.x >> 4), (float*)s_lds + RT_RSTACK * 16 + (threadIdx.x >> 4)};
-            if (closest)
-                trace_stream<false, STATS, PAIR, 16>(W, S, stk, s_pre, lo[r], n[r], wg, wn, fbn, fbl, ps);
-            else
-                trace_stream<true, STATS, PAIR, 16>(W, S, stk, s_pre, lo[r], n[r], wg, wn, fbn, fbl, ps);
-        } else {
-            rtk::QuadStack<RT_QSTACK, 64> stk{s_lds + (threadIdx.x >> 2), (float*)s_lds + RT_QSTACK * 64 + (threadIdx.x >> 2)};
-            if (closest)
-                trace_stream<false, STATS, PAIR, 4>(W, S, stk, s_pre, lo[r], n[r], wg, wn, fbn, fbl, ps);
-            else
-                trace_stream<true, STATS, PAIR, 4>(W, S, stk, s_pre, lo[r], n[r], wg, wn, fbn, fbl, ps);
-        }
-        flush_stats<STATS>(st, stats);
-        return;
-    }
     const int fb0 = 0, nbf = (int)gridDim.x;
     const int nbc = split_blocks(nbf, nc, na);
     const bool closest = b - fb0 < nbc;
@@ -874,6 +816,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_OC
     const int total = closest ? nc : na;
     int32_t* fbn = cnt + (closest ? C_FBC0 : C_FBA0) + par;  // walked exactly by k_step(i)
     rtk::RayRec* fbl = closest ? W.fb_c[par] : W.fb_a[par];
+    // The wave's queries are a stream (its 16-query chunks base = wg*16 + c*wn*16 in turn):
+    // each quad walks one, one trip per loop (rt_quad.h quad_visit), and as soon as
+    // RT_TRACE_REFILL quads are idle they all take the next queries, so a long walk holds
+    // up its own quad, not the wave's next 15 queries.
     if constexpr (G == 4) {
         rtk::QuadStack<RT_QSTACK, 64> stk{s_lds + (threadIdx.x >> 2), (float*)s_lds + RT_QSTACK * 64 + (threadIdx.x >> 2)};
         if (closest)
@@ -1592,8 +1538,6 @@ int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounces, cons
     if (const char* e = getenv("RT_ROW_BELOW")) row_below = atol(e);
     int tail_rows = RT_TAIL_ROWS;
     if (const char* e = getenv("RT_TAIL_ROWS")) tail_rows = atoi(e) != 0;
-    int heavy_rows = RT_HEAVY_ROWS;  // k_trace: the heavy class (predicted-long walks) by rows
-    if (const char* e = getenv("RT_HEAVY_ROWS")) heavy_rows = atoi(e) != 0;
     // (rows: one path per wave, its ~4 queries on the wave's 4 rows: shard 367 ms vs 2 / 3 paths
     // 373-378 / 373-375 at the same entry live count)
     int tail_p = tail_rows ? 1 : 2;
@@ -1708,15 +1652,15 @@ int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounces, cons
             for (int k = 0; k < 3; k++)
                 if (!La.tev[k][La.it]) HIPCHK(c, hipEventCreate(&La.tev[k][La.it]));
         if (T) HIPCHK(c, hipEventRecord(La.tev[0][La.it], La.s));
-        // walks by quads; or with heavy_rows the heavy class by rows; or (row_below) all by rows
-        const int gm = La.live < row_below ? 16 : (heavy_rows && heavy_calls > 0) ? 0 : 4;
+        // sparse launches (few live paths: the launch ends with its longest walk) walk with rows
+        const bool rows = La.live < row_below;
         const dim3 g(trace_blocks_of(La));
         if (SEQ)
-            hipLaunchKernelGGL((gm == 16 ? k_trace<true, false, 16> : gm == 0 ? k_trace<true, false, 0> : k_trace<true, false, 4>), g, dim3(threads), 0, La.s, W, par, stats);
+            hipLaunchKernelGGL((rows ? k_trace<true, false, 16> : k_trace<true, false, 4>), g, dim3(threads), 0, La.s, W, par, stats);
         else if (S)
-            hipLaunchKernelGGL((gm == 16 ? k_trace<true, true, 16> : gm == 0 ? k_trace<true, true, 0> : k_trace<true, true, 4>), g, dim3(threads), 0, La.s, W, par, stats);
+            hipLaunchKernelGGL((rows ? k_trace<true, true, 16> : k_trace<true, true, 4>), g, dim3(threads), 0, La.s, W, par, stats);
         else
-            hipLaunchKernelGGL((gm == 16 ? k_trace<false, true, 16> : gm == 0 ? k_trace<false, true, 0> : k_trace<false, true, 4>), g, dim3(threads), 0, La.s, W, par, stats);
+            hipLaunchKernelGGL((rows ? k_trace<false, true, 16> : k_trace<false, true, 4>), g, dim3(threads), 0, La.s, W, par, stats);
         if (T) HIPCHK(c, hipEventRecord(La.tev[1][La.it], La.s));
         HIPCHK(c, hipGetLastError());
         return RT_OK;
