@@ -69,10 +69,11 @@ struct alignas(128) Bvh4Node {
 };
 static_assert(sizeof(Bvh4Node) == 128, "Bvh4Node must be 128 B");
 // 16-wide search BVH (rt_scene.cpp build_bvh16, walked by 16-lane rows: rt_row.h): node
-// i is records [16 i, 16 i + 16) of Bvh4Child, 512 B, one record per lane of a row. A
-// node holds two levels of the 4-wide tree: the leaf children of a 4-wide node and the
-// children of its inner children; an inner record's ref is a 16-wide node index. Same
-// boxes, same leaves (<= 4 triangles), so the same hits.
+// i is records [16 i, 16 i + 16) of Bvh4Child, 512 B, one record per lane of a row, and
+// holds two levels of 4-wide node i: its leaf children and the children of its inner
+// children (an inner record's ref is a 4-wide node index, which is also its 16-wide node).
+// Same boxes, same leaves (<= 4 triangles), so the same hits; same item numbering, so a
+// walk may switch between quads and rows at any trip.
 #define RT_BVH16_W 16
 
 struct alignas(16) RtMat {

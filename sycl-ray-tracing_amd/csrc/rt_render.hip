@@ -672,9 +672,33 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_STEP_OCC
     flush_stats<STATS>(st, stats);
 }
 
+// A row's stack held in its wave's quad stacks (k_trace's drain, trace_stream): row k of a
+// wave uses the words of the wave's quads 4k .. 4k+3, entry e at depth e >> 2 of quad
+// 4k + (e & 3), so converting the wave's walks to rows needs no other LDS.
+struct RowInQuadStack {
+    static constexpr int CAP = 4 * RT_QSTACK;
+    uint32_t* r;  // the word of quad 4k, depth 0
+    float* k;
+    __device__ __forceinline__ uint32_t rec(int i) const { return r[(i >> 2) * 64 + (i & 3)]; }
+    __device__ __forceinline__ float key(int i) const { return k[(i >> 2) * 64 + (i & 3)]; }
+    __device__ __forceinline__ void set(int i, uint32_t rv, float kv)
+    {
+        r[(i >> 2) * 64 + (i & 3)] = rv;
+        k[(i >> 2) * 64 + (i & 3)] = kv;
+    }
+    __device__ __forceinline__ void set_rec(int i, uint32_t rv) { r[(i >> 2) * 64 + (i & 3)] = rv; }
+};
+
+#ifndef RT_DRAIN_ROWS
+#define RT_DRAIN_ROWS 4  // k_trace: once a wave's stream is out and at most this many quads still walk,
+                         // their walks continue as rows (rt_row.h); 0 = off
+#endif
+
 // k_trace's fast roles with per-quad refill (RT_TRACE_REFILL > 0): see k_trace.
 // G = lanes per query: 4 (quads over the 4-wide BVH, rt_quad.h) or 16 (rows over the 16-wide
-// BVH, rt_row.h: half the trips per walk; sparse launches, where the longest walk sets the end).
+// BVH, rt_row.h). With quads, the drain (the wave's stream out, its last long walks running
+// while the other quads idle) continues those walks as rows: same items, same stack entries
+// (the 16-wide BVH is numbered like the 4-wide one), half the trips per remaining level.
 template <bool ANY, bool STATS, bool PAIR, int G, class QSTK>
 __device__ __forceinline__ void trace_stream(const rtk::WaveView& W, const RtSceneView& S, QSTK& stk, const int* s_pre,
                                              int first, int total, int wg, int wn, int32_t* fbn, rtk::RayRec* fbl,
@@ -683,12 +707,43 @@ __device__ __forceinline__ void trace_stream(const rtk::WaveView& W, const RtSce
     static_assert(G == 4 || G == 16, "quads or rows");
     constexpr unsigned long long ALL_IDLE = G == 4 ? 0x1111111111111111ull : 0x0001000100010001ull;
     constexpr int REFILL = G == 4 ? RT_TRACE_REFILL : 1;  // idle groups that trigger a refill
-    const int lane = lane_id(), qd = lane / G, sub = lane & (G - 1);
+    const int lane = lane_id(), qd = lane / G;
+    int sub = lane & (G - 1);
     int cursor = 0;                     // the wave's next stream position (uniform)
     bool exhausted = wg * 16 >= total;  // (uniform)
     bool active = false;
     uint32_t target = 0;
     rtk::QState q;  // (its ray is the query's: a fallback record is rebuilt from q.o, q.d and target)
+    // a walk's end: its answer, or the exact walk's list; gs = lanes of the group walking it
+    auto finish = [&](int res, int gs) {
+        // a long walk: the path's next rays go to the heavy class (head of the next streams)
+        // (a row call covers two 4-wide levels: counted twice)
+        if (W.r_heavy && sub == 0 && (gs == 4 ? q.calls : 2 * q.calls) >= W.heavy_calls) W.r_heavy[target >> 3] = 1;
+        if (STATS && W.iterq && sub == 0 && W.iter < RT_MAX_TIMED_ITERS) {
+            // (RT_ITER_LOG: the launch's longest walk in quad_visit calls per role, and
+            // how many walks took more than 8)
+            int32_t* q2 = W.iterq + 2 * RT_MAX_TIMED_ITERS + 4 * W.iter;
+            atomicMax(q2 + (ANY ? 1 : 0), q.calls);
+            if (q.calls > 8) atomicAdd(q2 + 2, 1);
+        }
+        float t = 0.0f;
+        int k = 0;
+        // (rows: each quad of the row verifies alike; one counts)
+        if (res > 0 && !ANY && !rtk::quad_closest_answer(S, q, sub & 3, t, k, gs == 4 || sub == 0 ? ps : nullptr))
+            res = -1;
+        if (sub == 0) {
+            if (res > 0) {
+                if (ANY)
+                    rtk::finish_any(W, target, q.h.k == 1);
+                else
+                    rtk::finish_closest(W, target, q.o, q.d, t, k);
+            } else {  // the exact walk answers it (k_step(i)); the queue record again (o.w: slot)
+                fbl[atomicAdd(fbn, 1)] = rtk::RayRec{rtk::f4(q.o, rt_asfloat(target >> 3)),
+                                                     rtk::f4(q.d, rt_asfloat(target & 7u))};
+                atomicAdd(&W.r_park[target >> 3], 1);
+            }
+        }
+    };
     for (;;) {
         const unsigned long long bidle = __ballot(!active && sub == 0);
         if (!exhausted && (__popcll(bidle) >= REFILL || bidle == ALL_IDLE)) {
@@ -720,10 +775,12 @@ __device__ __forceinline__ void trace_stream(const rtk::WaveView& W, const RtSce
             exhausted = (wg + (cursor >> 4) * wn) * 16 >= total;
             if (STATS && lane == 0) ps->c[RT_STAT_REFILLS]++;
         }
-        if (!__any(active)) {
+        const unsigned long long bact = __ballot(active && sub == 0);
+        if (!bact) {
             if (exhausted) break;
             continue;
         }
+        if (G == 4 && W.drain_rows > 0 && exhausted && __popcll(bact) <= W.drain_rows) break;  // to rows (below)
         if (STATS) {  // SIMT slots of this trip: 16 quads, the active ones used
             if (active && sub == 0) ps->c[exhausted ? RT_STAT_DRAIN_VISITS : RT_STAT_QUAD_VISITS]++;
             if (lane == 0) ps->c[exhausted ? RT_STAT_DRAIN_SLOTS : RT_STAT_WAVE_SLOTS] += 64 / G;
@@ -737,31 +794,58 @@ __device__ __forceinline__ void trace_stream(const rtk::WaveView& W, const RtSce
             q.calls++;
             if (res != 0) {
                 active = false;
-                // a long walk: the path's next rays go to the heavy class (head of the next streams)
-                if (W.r_heavy && sub == 0 && q.calls >= W.heavy_calls) W.r_heavy[target >> 3] = 1;
-                if (STATS && W.iterq && sub == 0 && W.iter < RT_MAX_TIMED_ITERS) {
-                    // (RT_ITER_LOG: the launch's longest walk in quad_visit calls per role, and
-                    // how many walks took more than 8)
-                    int32_t* q2 = W.iterq + 2 * RT_MAX_TIMED_ITERS + 4 * W.iter;
-                    atomicMax(q2 + (ANY ? 1 : 0), q.calls);
-                    if (q.calls > 8) atomicAdd(q2 + 2, 1);
-                }
-                float t = 0.0f;
-                int k = 0;
-                // (rows: each quad of the row verifies alike; one counts)
-                if (res > 0 && !ANY && !rtk::quad_closest_answer(S, q, sub & 3, t, k, G == 4 || sub == 0 ? ps : nullptr))
-                    res = -1;
-                if (sub == 0) {
-                    if (res > 0) {
-                        if (ANY)
-                            rtk::finish_any(W, target, q.h.k == 1);
-                        else
-                            rtk::finish_closest(W, target, q.o, q.d, t, k);
-                    } else {  // the exact walk answers it (k_step(i)); the queue record again (o.w: slot)
-                        fbl[atomicAdd(fbn, 1)] = rtk::RayRec{rtk::f4(q.o, rt_asfloat(target >> 3)),
-                                                             rtk::f4(q.d, rt_asfloat(target & 7u))};
-                        atomicAdd(&W.r_park[target >> 3], 1);
-                    }
+                finish(res, G);
+            }
+        }
+    }
+    if constexpr (G == 4) {
+        // The drain as rows: the k-th walking quad of the wave (lane order) continues on row k.
+        const unsigned long long bact = __ballot(active && sub == 0);
+        if (!bact) return;
+        const int row = lane >> 4;
+        unsigned long long m = bact;
+        for (int i = 0; i < row; i++) m &= m - 1ull;
+        const int src = m ? __ffsll((long long)m) - 1 : 0;  // the walking quad's lane 0
+        const bool ract = m != 0;
+        // its state (quad-uniform) to the row's lanes
+        auto pf = [&](float v) { return __shfl(v, src); };
+        auto pi = [&](int v) { return __shfl(v, src); };
+        q.o = rtk::v3(pf(q.o.x), pf(q.o.y), pf(q.o.z));
+        q.d = rtk::v3(pf(q.d.x), pf(q.d.y), pf(q.d.z));
+        for (int i = 0; i < 3; i++) q.rb.inv[i] = pf(q.rb.inv[i]), q.rb.oi[i] = pf(q.rb.oi[i]);
+        q.h.t = pf(q.h.t), q.h.t2 = pf(q.h.t2), q.h.k = pi(q.h.k), q.h.leaf = pi(q.h.leaf), q.h.prim = pi(q.h.prim);
+        q.h.tie = pi(q.h.tie ? 1 : 0) != 0, q.h.ovf = pi(q.h.ovf ? 1 : 0) != 0;
+        q.sp = pi(q.sp), q.cur = pi(q.cur), q.calls = pi(q.calls);
+        target = (uint32_t)pi((int)target);
+        // its stack (<= RT_QSTACK entries), through registers: read everything, then write
+        sub = lane & 15;
+        const int wq = (int)(threadIdx.x >> 6) * 16;  // the wave's first quad in the block
+        uint32_t* qr = stk.r - (threadIdx.x >> 2) + wq;  // word of the wave's quad 0, depth 0
+        float* qk = stk.k - (threadIdx.x >> 2) + wq;
+        const int sq = src >> 2;
+        uint32_t r0 = 0, r1 = 0;
+        float k0 = 0.0f, k1 = 0.0f;
+        if (ract && sub < q.sp) r0 = qr[sub * 64 + sq], k0 = qk[sub * 64 + sq];
+        if (ract && sub + 16 < q.sp) r1 = qr[(sub + 16) * 64 + sq], k1 = qk[(sub + 16) * 64 + sq];
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        RowInQuadStack rs{qr + 4 * row, qk + 4 * row};
+        if (ract && sub < q.sp) rs.set(sub, r0, k0);
+        if (ract && sub + 16 < q.sp) rs.set(sub + 16, r1, k1);
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        active = ract;
+        while (__any(active)) {
+            if (STATS) {
+                if (active && sub == 0) ps->c[RT_STAT_DRAIN_VISITS]++;
+                if (lane == 0) ps->c[RT_STAT_DRAIN_SLOTS] += 4;
+            }
+            if (active) {
+                const int res = rtk::row_visit<ANY, RT_VISIT_DESCEND>(S, q, rs, sub, ps);
+                q.calls++;
+                if (res != 0) {
+                    active = false;
+                    finish(res, 16);
                 }
             }
         }
@@ -1538,6 +1622,8 @@ int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounces, cons
     if (const char* e = getenv("RT_ROW_BELOW")) row_below = atol(e);
     int tail_rows = RT_TAIL_ROWS;
     if (const char* e = getenv("RT_TAIL_ROWS")) tail_rows = atoi(e) != 0;
+    int drain_rows = RT_DRAIN_ROWS;  // k_trace: a drain's walks continue as rows (trace_stream)
+    if (const char* e = getenv("RT_DRAIN_ROWS")) drain_rows = std::max(0, std::min(4, atoi(e)));
     // (rows: one path per wave, its ~4 queries on the wave's 4 rows: shard 367 ms vs 2 / 3 paths
     // 373-378 / 373-375 at the same entry live count)
     int tail_p = tail_rows ? 1 : 2;
@@ -1609,6 +1695,7 @@ int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounces, cons
         W.budget = b->budget;
         W.counters = La.cnt;
         W.tail_paths = tail_p;
+        W.drain_rows = drain_rows;
         W.force_fb = force_fb;
         W.iterq = (S && iter_log && l == 0) ? (int32_t*)b->iterq.p : nullptr;
         La.lists[0] = (int32_t*)W.act_in;

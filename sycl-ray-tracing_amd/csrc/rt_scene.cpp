@@ -1306,49 +1306,35 @@ static int bvh4_top_first(std::vector<Bvh4Node>& b4, int k)
     return (int)bfs.size();
 }
 
-// The 16-wide form of the 4-wide tree: node = a 4-wide node of even depth, its records the
-// node's leaf children and the children of its inner children (up to 16; empty slots
-// cnt -1 with an inverted box). An inner record's ref becomes the 16-wide node built for
-// that 4-wide node (depth + 2). Boxes and leaves are copied unchanged.
+// The 16-wide form of the 4-wide tree, index for index: 16-wide node i holds 4-wide node
+// i's leaf children and the children of its inner children (up to 16; empty slots cnt -1
+// with an inverted box), an inner record's ref being the 4-wide node index (= its 16-wide
+// node). Any item of a 4-wide walk is an item of a 16-wide walk, so a quad walk's stack can
+// be continued by a row (rt_render.hip trace_stream). Boxes and leaves copied unchanged.
 static void build_bvh16(const std::vector<Bvh4Node>& b4, std::vector<Bvh4Child>& b16)
 {
-    b16.clear();
-    if (b4.empty()) return;
     Bvh4Child empty{};
     for (int a = 0; a < 3; a++) empty.lo[a] = INFINITY, empty.hi[a] = -INFINITY;
     empty.ref = 0;
     empty.cnt = -1;
-    struct Task {
-        int n4, n16;
-    };
-    std::vector<Task> st{{0, 0}};
-    b16.assign(RT_BVH16_W, empty);
-    while (!st.empty()) {
-        const Task t = st.back();
-        st.pop_back();
-        Bvh4Child rec[RT_BVH16_W];
-        int m = 0;
-        auto take = [&](const Bvh4Child& c) {
-            Bvh4Child r = c;
-            if (r.cnt == 0) {  // an inner 4-wide node two levels down: its own 16-wide node
-                const int id = (int)(b16.size() / RT_BVH16_W);
-                b16.insert(b16.end(), RT_BVH16_W, empty);
-                st.push_back({c.ref, id});
-                r.ref = id;
-            }
-            rec[m++] = r;
-        };
-        for (const Bvh4Child& c : b4[t.n4].ch) {
-            if (c.cnt < 0) continue;
-            if (c.cnt > 0) {
-                take(c);
-            } else {
-                for (const Bvh4Child& g : b4[c.ref].ch)
-                    if (g.cnt >= 0) take(g);
+    b16.assign(b4.size() * RT_BVH16_W, empty);
+    const int n = (int)b4.size();
+    const int nw = worker_count();
+    parallel_for(nw, nw, [&](int w) {
+        for (int i = (int)((long)n * w / nw); i < (int)((long)n * (w + 1) / nw); i++) {
+            Bvh4Child* rec = &b16[(size_t)i * RT_BVH16_W];
+            int m = 0;
+            for (const Bvh4Child& c : b4[i].ch) {
+                if (c.cnt < 0) continue;
+                if (c.cnt > 0) {
+                    rec[m++] = c;
+                } else {
+                    for (const Bvh4Child& g : b4[c.ref].ch)
+                        if (g.cnt >= 0) rec[m++] = g;
+                }
             }
         }
-        for (int i = 0; i < RT_BVH16_W; i++) b16[(size_t)t.n16 * RT_BVH16_W + i] = i < m ? rec[i] : empty;
-    }
+    });
 }
 
 void build_search_bvh(FlatBvh& out)

@@ -276,7 +276,8 @@ def test_gpu_schedules_bit_identical(monkeypatch):
     sky = scenes.make_sky("L")
     W, H, spp, nb = 640, 480, 2, 8
 
-    def render(lanes, tail, off=0, stride=1, heavy=6, enter=2.0, spec_cam=1, rows=1, row_below=0):
+    def render(lanes, tail, off=0, stride=1, heavy=6, enter=2.0, spec_cam=1, rows=1, row_below=0, drain=4):
+        monkeypatch.setenv("RT_DRAIN_ROWS", str(drain))
         monkeypatch.setenv("RT_TAIL_ROWS", str(rows))
         monkeypatch.setenv("RT_ROW_BELOW", str(row_below))
         monkeypatch.setenv("RT_LANES", str(lanes))
@@ -317,8 +318,10 @@ def test_gpu_schedules_bit_identical(monkeypatch):
         got = render(lanes, tail, spec_cam=0)
         np.testing.assert_array_equal(got.view(np.uint32), base.view(np.uint32), err_msg=f"spec_cam=0 lanes={lanes}")
     # the walks by quads or by rows (rt_row.h) in the tail kernel, and rows in every k_trace launch
-    for rows, row_below, tail, enter in ((0, 0, 2, 2.0), (1, 0, 1, 1000.0), (1, 1 << 30, 1, 2.0), (0, 1 << 30, 4, 2.0)):
-        got = render(3, tail, enter=enter, rows=rows, row_below=row_below)
+    # (and a k_trace drain continuing its quad walks as rows, or not; 1 walk at most, or 4)
+    for rows, row_below, tail, enter, drain in ((0, 0, 2, 2.0, 0), (1, 0, 1, 1000.0, 1), (1, 1 << 30, 1, 2.0, 4),
+                                                (0, 1 << 30, 4, 2.0, 0), (1, 0, 0, 2.0, 4), (1, 0, 0, 2.0, 1)):
+        got = render(3, tail, enter=enter, rows=rows, row_below=row_below, drain=drain)
         np.testing.assert_array_equal(got.view(np.uint32), base.view(np.uint32),
                                       err_msg=f"rows={rows} row_below={row_below} tail={tail}")
 
