@@ -1821,13 +1821,23 @@ int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounces, cons
     };
     for (int l = 0; l < nl; l++)
         if (int r = issue(L[l])) return r;
+    // The host serves whichever lane's readback has completed (hipEventQuery), so a lane whose
+    // batch is done is refilled at once instead of idling while the host blocks on another
+    // lane's event (blocking in lane order left lanes idle 17-34 ms of a 367-ms cfg4 8-way
+    // shard: profiles/r04e_tl.json).
     for (;;) {
-        bool any = false;
+        bool any = false, moved = false;
         for (int l = 0; l < nl; l++) {
             WaveLane& La = L[l];
-            if (La.await)
+            if (La.await) {
+                any = true;
+                const hipError_t q = hipEventQuery(La.ev);
+                if (q == hipErrorNotReady) continue;
+                HIPCHK(c, q);
                 if (int r = process(La)) return r;
-            if (!La.done) {
+                moved = true;
+            }
+            if (!La.done && !La.await) {
                 if (La.it >= max_iters) {
                     HIPCHK(c, hipStreamSynchronize(La.s));
                     return rt_fail(c, RT_ERR_STATE, "render: wavefront loop did not drain in " +
@@ -1835,10 +1845,11 @@ int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounces, cons
                                                             std::to_string(b->budget) + ")");
                 }
                 if (int r = issue(La)) return r;
-                any = true;
+                any = moved = true;
             }
         }
         if (!any) break;
+        if (!moved) std::this_thread::yield();
     }
     for (int l = 0; l < nl; l++) {  // each lane's pixels tone-mapped after its last step
         hipLaunchKernelGGL(k_tonemap, dim3((L[l].n + threads - 1) / threads), dim3(threads), 0, L[l].s, L[l].W);
