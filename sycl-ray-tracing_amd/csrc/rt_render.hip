@@ -1622,6 +1622,7 @@ int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounces, cons
     if (const char* e = getenv("RT_ROW_BELOW")) row_below = atol(e);
     int tail_rows = RT_TAIL_ROWS;
     if (const char* e = getenv("RT_TAIL_ROWS")) tail_rows = atoi(e) != 0;
+    const bool host_blocking = getenv("RT_HOST_BLOCKING") && atoi(getenv("RT_HOST_BLOCKING")) != 0;  // (A/B: round 3's loop)
     int drain_rows = RT_DRAIN_ROWS;  // k_trace: a drain's walks continue as rows (trace_stream)
     if (const char* e = getenv("RT_DRAIN_ROWS")) drain_rows = std::max(0, std::min(4, atoi(e)));
     // (rows: one path per wave, its ~4 queries on the wave's 4 rows: shard 367 ms vs 2 / 3 paths
@@ -1831,7 +1832,7 @@ int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounces, cons
             WaveLane& La = L[l];
             if (La.await) {
                 any = true;
-                const hipError_t q = hipEventQuery(La.ev);
+                const hipError_t q = host_blocking ? hipEventSynchronize(La.ev) : hipEventQuery(La.ev);
                 if (q == hipErrorNotReady) continue;
                 HIPCHK(c, q);
                 if (int r = process(La)) return r;
