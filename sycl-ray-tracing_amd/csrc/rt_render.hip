@@ -690,8 +690,10 @@ struct RowInQuadStack {
 };
 
 #ifndef RT_DRAIN_ROWS
-#define RT_DRAIN_ROWS 4  // k_trace: once a wave's stream is out and at most this many quads still walk,
-                         // their walks continue as rows (rt_row.h); 0 = off
+#define RT_DRAIN_ROWS 2  // k_trace: once a wave's stream is out and at most this many quads still walk,
+                         // their walks continue as rows (rt_row.h); 0 = off. cfg4 8-way shard, one
+                         // MI355X (profiles/r04i_drain_probe.json): off / 4 / 2 -> 370-373 / 362.6-362.9 /
+                         // 360.5-360.7 ms, cfg2 148.0 / 145.3-145.9 / 146.0 ms
 #endif
 
 // k_trace's fast roles with per-quad refill (RT_TRACE_REFILL > 0): see k_trace.
@@ -1825,7 +1827,8 @@ int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounces, cons
     // The host serves whichever lane's readback has completed (hipEventQuery), so a lane whose
     // batch is done is refilled at once instead of idling while the host blocks on another
     // lane's event (blocking in lane order left lanes idle 17-34 ms of a 367-ms cfg4 8-way
-    // shard: profiles/r04e_tl.json).
+    // shard: profiles/r04e_tl.json; 379.5-380.2 -> 370.5-373.2 ms, cfg2 148.5-149.7 -> 148.0,
+    // profiles/r04i_drain_probe.json).
     for (;;) {
         bool any = false, moved = false;
         for (int l = 0; l < nl; l++) {
