@@ -690,10 +690,11 @@ struct RowInQuadStack {
 };
 
 #ifndef RT_DRAIN_ROWS
-#define RT_DRAIN_ROWS 2  // k_trace: once a wave's stream is out and at most this many quads still walk,
+#define RT_DRAIN_ROWS 3  // k_trace: once a wave's stream is out and at most this many quads still walk,
                          // their walks continue as rows (rt_row.h); 0 = off. cfg4 8-way shard, one
-                         // MI355X (profiles/r04i_drain_probe.json): off / 4 / 2 -> 370-373 / 362.6-362.9 /
-                         // 360.5-360.7 ms, cfg2 148.0 / 145.3-145.9 / 146.0 ms
+                         // MI355X (profiles/r04i_drain_probe.json, r04j_probe.json): off / 4 / 3 / 2 / 1 ->
+                         // 370-373 / 362.6-362.9 / 359.9-361.4 / 360.5-363.6 / 366.5-367.3 ms, cfg2 148.0 /
+                         // 145.3-145.9 / 145.1-145.4 / 145.6-146.0 / 147.1-147.6 ms
 #endif
 
 // k_trace's fast roles with per-quad refill (RT_TRACE_REFILL > 0): see k_trace.
