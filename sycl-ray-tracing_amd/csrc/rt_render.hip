@@ -36,6 +36,7 @@
 #include "rt_wave.h"
 #include "rt_quad.h"
 #include "rt_row.h"
+#include "rt_octet.h"
 
 #define HIPCHK(ctx, expr)                                                                         \
     do {                                                                                          \
@@ -491,6 +492,89 @@ __device__ __forceinline__ void walk_done(const rtk::WaveView& W, int par, uint3
     W.done[par][j] = (int32_t)(target >> 3);
 }
 
+#ifndef RT_EXACT_OCTET
+#define RT_EXACT_OCTET 1  // k_step's exact walks: 8 lanes per query (rt_octet.h); 0: one lane per query
+#endif
+#if RT_EXACT_OCTET
+// Exact octree walks of k_step(i) (par = i & 1), one octet of lanes per query (rt_octet.h):
+// the walks parked by k_step(i - 1) (PARK[par ^ 1], the first n_res tickets), then the
+// fallbacks of k_trace(i) (FB[par]). ANY selects the occlusion walk.
+template <bool ANY>
+__device__ void exact_octets(const rtk::WaveView& W, int par, uint32_t* lds, int lane, int n_res, int total,
+                             rtk::Stats* st)
+{
+    rtk::OctRing w = rtk::oct_ring(lds);
+    const int sub = lane_id() & 7;
+    uint32_t* spr = W.spill_r + (size_t)(lane & ~7) * RT_STACK_CAP;  // the leader lane's spill area
+    float* spk = W.spill_k + (size_t)(lane & ~7) * RT_STACK_CAP;
+    const rtk::RayRec* fb = ANY ? W.fb_a[par] : W.fb_c[par];
+    int32_t* ticket = W.counters + (ANY ? C_TK_EXACT_A : C_TK_EXACT_C);
+    int32_t* parked = W.counters + (ANY ? C_PARKA0 : C_PARKC0) + par;
+    rtk::TravG T;
+    bool has = false, drained = false;  // (octet-uniform)
+    uint32_t target = 0;
+    auto done = [&]() {
+        if (sub == 0) {
+            if (ANY)
+                rtk::finish_any(W, target, T.hit);  // (false, or the brute-force answer)
+            else
+                rtk::finish_closest(W, target, T.o, T.d, T.best_t, T.best_k);
+            walk_done(W, par, target);
+        }
+    };
+    for (;;) {
+        const unsigned long long bneed = __ballot(!has && sub == 0);
+        const int nneed = __popcll(bneed);
+        if (!drained && (nneed >= RT_REFILL / 8 || nneed == 8)) {
+            int base = 0;
+            if (lane_id() == 0) base = atomicAdd(ticket, nneed);
+            base = __shfl(base, 0);
+            if (base + nneed >= total) drained = true;
+            if (!has) {
+                const int idx = base + __popcll(bneed & ((1ull << rtk::oct_lane0()) - 1ull));
+                if (idx < n_res) {
+                    target = ANY ? rtk::octa_resume(W.S, &W.park_a[par ^ 1][idx], T, w, sub)
+                                 : rtk::octc_resume(W.S, &W.park_c[par ^ 1][idx], T, w, sub);
+                    has = true;
+                } else if (idx < total) {
+                    const rtk::RayRec r = fb[idx - n_res];
+                    target = (rt_asuint(r.o.w) << 3) | rt_asuint(r.d.w);
+                    if (st && sub == 0) st->c[RT_STAT_FALLBACK]++;
+                    has = rtk::octg_setup(W.S, T, rtk::v3of(r.o), rtk::v3of(r.d), st, ANY, sub);
+                    if (!has) done();
+                }
+            }
+        }
+        if (!__any(has)) {
+            if (drained) break;
+            continue;
+        }
+        if (has) {
+            if (ANY)
+                rtk::octa_node(W.S, T, w, spr, sub, st);
+            else
+                rtk::octc_node(W.S, T, w, spr, spk, sub, st);
+            if (T.mode == rtk::TM_DONE) {
+                done();
+                has = false;
+            } else if (T.steps >= W.budget && (ANY ? rtk::octa_parkable(T) : rtk::octc_parkable(T))) {
+                int ps = 0;
+                if (sub == 0) ps = atomicAdd(parked, 1);
+                ps = __shfl(ps, rtk::oct_lane0());
+                if (ps < W.park_cap) {
+                    if (ANY)
+                        rtk::octa_park(T, w, target, &W.park_a[par][ps], sub);
+                    else
+                        rtk::octc_park(T, w, target, &W.park_c[par][ps], sub);
+                    has = false;
+                } else {
+                    T.steps = 0;  // park pool full: keep going
+                }
+            }
+        }
+    }
+}
+#else
 // Exact octree walks of k_step(i) (par = i & 1): the walks parked by k_step(i - 1)
 // (PARK[par ^ 1], the first n_res tickets), then the fallbacks of k_trace(i) (FB[par]).
 __device__ void exact_closest(const rtk::WaveView& W, int par, uint32_t* lds, int lane, int n_res, int total,
@@ -608,6 +692,8 @@ __device__ void exact_any(const rtk::WaveView& W, int par, uint32_t* lds, int la
     }
 }
 
+#endif
+
 // Path step of iteration i (par = i & 1): resolve, shade, next sample, for
 // every live path not waiting on an exact walk; the first blocks instead run
 // the exact octree walks of this iteration's fallbacks and of the walks parked
@@ -629,22 +715,31 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_STEP_OCC
     if (STATS)
         for (int i = 0; i < RT_STAT_COUNT; i++) st.c[i] = 0;
     rtk::Stats* ps = STATS ? &st : nullptr;
-    // exact roles: 64 walks per block to start with (16 per wave), at most half of the
+    // exact roles: 32 walks per block to start with (8 octets per wave), at most half of the
     // spill lanes and a quarter of the grid each
     const int nrc = min(cnt[C_PARKC0 + (par ^ 1)], W.park_cap), nra = min(cnt[C_PARKA0 + (par ^ 1)], W.park_cap);
     const int ec = nrc + cnt[C_FBC0 + par], ea = nra + cnt[C_FBA0 + par];
     // (the host launches >= 3 blocks, so both exact roles and the path step each get one:
     // with gridDim 3, half = 1; above, the exact roles take at most half of the grid)
     const int half = min(W.spill_lanes / 512, max(1, (int)gridDim.x / 4));
-    const int nbe_c = min(half, (ec + 63) / 64), nbe_a = min(half, (ea + 63) / 64);
+    constexpr int WPB = RT_EXACT_OCTET ? 32 : 64;  // walks per block at once (octets / lanes)
+    const int nbe_c = min(half, (ec + WPB - 1) / WPB), nbe_a = min(half, (ea + WPB - 1) / WPB);
     const int b = (int)blockIdx.x;
     if (b < nbe_c) {
+#if RT_EXACT_OCTET
+        exact_octets<false>(W, par, s_lds, b * 256 + (int)threadIdx.x, nrc, ec, ps);
+#else
         exact_closest(W, par, s_lds, b * 256 + (int)threadIdx.x, nrc, ec, ps);
+#endif
         flush_stats<STATS>(st, stats);
         return;
     }
     if (b < nbe_c + nbe_a) {
+#if RT_EXACT_OCTET
+        exact_octets<true>(W, par, s_lds, (W.spill_lanes / 512 + b - nbe_c) * 256 + (int)threadIdx.x, nra, ea, ps);
+#else
         exact_any(W, par, s_lds, (W.spill_lanes / 512 + b - nbe_c) * 256 + (int)threadIdx.x, nra, ea, ps);
+#endif
         flush_stats<STATS>(st, stats);
         return;
     }
@@ -744,6 +839,8 @@ __device__ __forceinline__ void trace_stream(const rtk::WaveView& W, const RtSce
                 fbl[atomicAdd(fbn, 1)] = rtk::RayRec{rtk::f4(q.o, rt_asfloat(target >> 3)),
                                                      rtk::f4(q.d, rt_asfloat(target & 7u))};
                 atomicAdd(&W.r_park[target >> 3], 1);
+                if (STATS && W.iterq && W.iter < RT_MAX_TIMED_ITERS)
+                    atomicAdd(W.iterq + 2 * RT_MAX_TIMED_ITERS + 4 * W.iter + 3, 1);  // (RT_ITER_LOG: fallbacks)
             }
         }
     };
@@ -1878,7 +1975,8 @@ int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounces, cons
         if (FILE* f = fopen((std::string(iter_log) + ".counts").c_str(), "w")) {
             const int32_t* h2 = hq.data() + 2 * RT_MAX_TIMED_ITERS;
             for (int i = 0; i <= L[0].it && i < RT_MAX_TIMED_ITERS; i++)
-                fprintf(f, "%d %d %d %d %d %d\n", i, hq[2 * i], hq[2 * i + 1], h2[4 * i], h2[4 * i + 1], h2[4 * i + 2]);
+                fprintf(f, "%d %d %d %d %d %d %d\n", i, hq[2 * i], hq[2 * i + 1], h2[4 * i], h2[4 * i + 1], h2[4 * i + 2],
+                        h2[4 * i + 3]);
             fclose(f);
         }
     }

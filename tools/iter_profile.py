@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--world", type=int, default=1)
     ap.add_argument("--lanes", type=int, default=1)
     ap.add_argument("--out", default="gpurun_out/iter")
+    ap.add_argument("--raw", action="store_true", help="add the per-iteration arrays")
     args = ap.parse_args()
     os.makedirs(os.path.dirname(args.out) or ".", exist_ok=True)
     prefix = f"{args.out}_{args.config}_w{args.world}"
@@ -75,6 +76,10 @@ def main():
     # the tail launch: rounds of its longest pool loop, 100 MHz ticks / 16 in steps and in walks (summed over waves)
     ti = int(cnt.shape[0]) - 1
     out["tail_row"] = [int(v) for v in cnt[ti]] if cnt.shape[0] > n_it else None
+    if args.raw:  # per-iteration arrays: live slots, queries, fallbacks (stats render), trace / step ms (timed)
+        out["raw"] = {"live": [int(v) for v in live], "queries": [int(v) for v in cnt[:n_it, 1]],
+                      "fallbacks": [int(v) for v in cnt[:n_it, 6]] if cnt.shape[1] > 6 else None,
+                      "trace_ms": [round(float(v), 4) for v in ms[:, 1]], "step_ms": [round(float(v), 4) for v in ms[:, 2]]}
     print(json.dumps(out))
 
 
