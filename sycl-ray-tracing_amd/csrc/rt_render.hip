@@ -37,7 +37,6 @@
 #include "rt_quad.h"
 #include "rt_row.h"
 #include "rt_octet.h"
-#include "rt_coop.h"
 
 #define HIPCHK(ctx, expr)                                                                         \
     do {                                                                                          \
@@ -785,26 +784,6 @@ struct RowInQuadStack {
     __device__ __forceinline__ void set_rec(int i, uint32_t rv) { r[(i >> 2) * 64 + (i & 3)] = rv; }
 };
 
-// A walk's state (quad- or row-uniform) from the group whose lane 0 is src, to this lane.
-__device__ __forceinline__ void take_walk(rtk::QState& q, uint32_t& target, int src)
-{
-    auto pf = [&](float v) { return __shfl(v, src); };
-    auto pi = [&](int v) { return __shfl(v, src); };
-    q.o = rtk::v3(pf(q.o.x), pf(q.o.y), pf(q.o.z));
-    q.d = rtk::v3(pf(q.d.x), pf(q.d.y), pf(q.d.z));
-    for (int i = 0; i < 3; i++) q.rb.inv[i] = pf(q.rb.inv[i]), q.rb.oi[i] = pf(q.rb.oi[i]);
-    q.h.t = pf(q.h.t), q.h.t2 = pf(q.h.t2), q.h.k = pi(q.h.k), q.h.leaf = pi(q.h.leaf), q.h.prim = pi(q.h.prim);
-    q.h.tie = pi(q.h.tie ? 1 : 0) != 0, q.h.ovf = pi(q.h.ovf ? 1 : 0) != 0;
-    q.sp = pi(q.sp), q.cur = pi(q.cur), q.calls = pi(q.calls);
-    target = (uint32_t)pi((int)target);
-}
-
-#ifndef RT_COOP
-#define RT_COOP 3  // a wave's last walk by its four rows (rt_coop.h): bit 0 in k_tail rounds, bit 1 in k_trace drains
-#endif
-#ifndef RT_COOP_TRACE
-#define RT_COOP_TRACE 1  // (0: k_trace without the code)
-#endif
 #ifndef RT_DRAIN_ROWS
 #define RT_DRAIN_ROWS 3  // k_trace: once a wave's stream is out and at most this many quads still walk,
                          // their walks continue as rows (rt_row.h); 0 = off. cfg4 8-way shard, one
@@ -929,7 +908,15 @@ __device__ __forceinline__ void trace_stream(const rtk::WaveView& W, const RtSce
         const int src = m ? __ffsll((long long)m) - 1 : 0;  // the walking quad's lane 0
         const bool ract = m != 0;
         // its state (quad-uniform) to the row's lanes
-        take_walk(q, target, src);
+        auto pf = [&](float v) { return __shfl(v, src); };
+        auto pi = [&](int v) { return __shfl(v, src); };
+        q.o = rtk::v3(pf(q.o.x), pf(q.o.y), pf(q.o.z));
+        q.d = rtk::v3(pf(q.d.x), pf(q.d.y), pf(q.d.z));
+        for (int i = 0; i < 3; i++) q.rb.inv[i] = pf(q.rb.inv[i]), q.rb.oi[i] = pf(q.rb.oi[i]);
+        q.h.t = pf(q.h.t), q.h.t2 = pf(q.h.t2), q.h.k = pi(q.h.k), q.h.leaf = pi(q.h.leaf), q.h.prim = pi(q.h.prim);
+        q.h.tie = pi(q.h.tie ? 1 : 0) != 0, q.h.ovf = pi(q.h.ovf ? 1 : 0) != 0;
+        q.sp = pi(q.sp), q.cur = pi(q.cur), q.calls = pi(q.calls);
+        target = (uint32_t)pi((int)target);
         // its stack (<= RT_QSTACK entries), through registers: read everything, then write
         sub = lane & 15;
         const int wq = (int)(threadIdx.x >> 6) * 16;  // the wave's first quad in the block
@@ -961,21 +948,6 @@ __device__ __forceinline__ void trace_stream(const rtk::WaveView& W, const RtSce
                     finish(res, 16);
                 }
             }
-#if RT_COOP_TRACE
-            const unsigned long long brow = __ballot(active && sub == 0);
-            if ((W.coop & 2) && __popcll(brow) == 1) {
-                // the wave's last walk: its four rows walk it together (rt_coop.h), on its row's stack
-                const int s0 = __ffsll((long long)brow) - 1;
-                take_walk(q, target, s0);
-                RowInQuadStack cs{qr + 4 * (s0 >> 4), qk + 4 * (s0 >> 4)};
-                int trips = 0;
-                const int res = rtk::coop_walk<ANY>(S, q, cs, ps, trips);
-                q.calls += trips;
-                sub = lane;  // (finish: one writer, lane 0)
-                finish(res, 16);
-                return;
-            }
-#endif
         }
     }
 }
@@ -1256,32 +1228,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TAIL_OCC
                     exact = !ok;
                 }
             }
-            if constexpr (G == 16) {
-                const unsigned long long brow = __ballot(act && sub == 0);
-                // (not while a finished walk of this trip still needs its exact walk: that lane's q)
-                if ((W.coop & 1) && next >= nq && __popcll(brow) == 1 && !__any(exact)) {
-                    // the round's last walk: the wave's four rows walk it together (rt_coop.h),
-                    // on its row's stack; lane 0 writes the answer
-                    const int s0 = __ffsll((long long)brow) - 1;
-                    take_walk(q, target, s0);
-                    l = __shfl(l, s0);
-                    const int sr = (int)(threadIdx.x >> 6) * 4 + (s0 >> 4);
-                    STK cs{s_stk + sr, (float*)s_stk + SCAP * GPB + sr};
-                    int trips = 0;
-                    const int res = l ? rtk::coop_walk<true>(S, q, cs, ps, trips) : rtk::coop_walk<false>(S, q, cs, ps, trips);
-                    float t = 0.0f;
-                    int k = 0;
-                    const bool ok = res > 0 && (l == 1 || rtk::quad_closest_answer(S, q, lane & 3, t, k, lane == 0 ? ps : nullptr));
-                    if (ok && lane == 0) {
-                        if (l == 0)
-                            rtk::finish_closest(W, target, q.o, q.d, t, k);
-                        else
-                            rtk::finish_any(W, target, q.h.k == 1);
-                    }
-                    exact = !ok && lane == 0;
-                    act = false;
-                }
-            }
             if (exact && sub == 0) {  // the exact octree walk, to completion
                 if (STATS) st.c[RT_STAT_FALLBACK]++;
                 xs.f = stk;
@@ -1424,36 +1370,6 @@ __global__ __launch_bounds__(256) void k_query_row(RtSceneView S, const float4_*
         int k = -1;
         const bool ok = res > 0 && (ANY || rtk::quad_closest_answer(S, qs, sub & 3, t, k, nullptr));
         if (sub == 0) {
-            if (ANY) {
-                out_t[i] = ok ? (float)(qs.h.k == 1 ? 1 : 0) : -2.0f;
-                out_k[i] = 0;
-            } else {
-                out_t[i] = ok ? t : -2.0f;
-                out_k[i] = ok ? k : -2;
-            }
-        }
-    }
-}
-
-// One query per wave, its four rows walking it together from the start (rt_coop.h; the
-// product runs coop_walk only on a wave's last walk). Answers as k_query_row.
-template <bool ANY>
-__global__ __launch_bounds__(256) void k_query_coop(RtSceneView S, const float4_* __restrict__ rays,
-                                                    float* __restrict__ out_t, int* __restrict__ out_k, int n)
-{
-    __shared__ uint32_t s_lds[2 * RT_RSTACK * 4];
-    const int w = (int)(threadIdx.x >> 6), lane = (int)(threadIdx.x & 63);
-    rtk::QuadStack<RT_RSTACK, 4> stk{s_lds + w, (float*)s_lds + RT_RSTACK * 4 + w};
-    const int stride = (int)(gridDim.x * blockDim.x) >> 6;
-    for (int i = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6); i < n; i += stride) {
-        rtk::QState qs;
-        int res = 1, trips = 0;
-        if (rtk::qstate_begin<ANY>(qs, rtk::v3of(rays[2 * i]), rtk::v3of(rays[2 * i + 1]), lane, nullptr))
-            res = rtk::coop_walk<ANY>(S, qs, stk, nullptr, trips);
-        float t = -1.0f;
-        int k = -1;
-        const bool ok = res > 0 && (ANY || rtk::quad_closest_answer(S, qs, lane & 3, t, k, nullptr));
-        if (lane == 0) {
             if (ANY) {
                 out_t[i] = ok ? (float)(qs.h.k == 1 ? 1 : 0) : -2.0f;
                 out_k[i] = 0;
@@ -1828,8 +1744,6 @@ int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounces, cons
     if (const char* e = getenv("RT_TAIL_ROWS")) tail_rows = atoi(e) != 0;
     const bool host_blocking = getenv("RT_HOST_BLOCKING") && atoi(getenv("RT_HOST_BLOCKING")) != 0;  // (A/B: round 3's loop)
     int drain_rows = RT_DRAIN_ROWS;  // k_trace: a drain's walks continue as rows (trace_stream)
-    int coop = RT_COOP;              // a wave's last walk by its four rows (rt_coop.h)
-    if (const char* e = getenv("RT_COOP")) coop = atoi(e) & 3;
     if (const char* e = getenv("RT_DRAIN_ROWS")) drain_rows = std::max(0, std::min(4, atoi(e)));
     // (rows: one path per wave, its ~4 queries on the wave's 4 rows: shard 367 ms vs 2 / 3 paths
     // 373-378 / 373-375 at the same entry live count)
@@ -1903,7 +1817,6 @@ int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounces, cons
         W.counters = La.cnt;
         W.tail_paths = tail_p;
         W.drain_rows = drain_rows;
-        W.coop = coop;
         W.force_fb = force_fb;
         W.iterq = (S && iter_log && l == 0) ? (int32_t*)b->iterq.p : nullptr;
         La.lists[0] = (int32_t*)W.act_in;
@@ -2449,12 +2362,12 @@ extern "C" int rt_device_libm(int device, int fn, const float* in, const float* 
 
 // Search-BVH query micro-benchmark: rays[n][8] (origin xyz _, direction xyz _),
 // mode bit 0 = any (else closest), bits 1.. = walk variant (0-1 one lane, 2-3 lane + spill,
-// 4-5 quads, 6-7 quads at 8 waves/SIMD, 8-9 rows, 10-11 a wave's four rows per query);
+// 4-5 quads, 6-7 quads at 8 waves/SIMD, 8-9 rows);
 // reps timed launches (HIP events), mean ms per launch into *ms.
 extern "C" int rt_device_queries(rt_context* c, int mode, const float* rays, int n, int reps, float* out_t,
                                  int* out_k, double* ms)
 {
-    if (!c || !c->backend || n <= 0 || reps < 1 || mode < 0 || mode > 11) return RT_ERR_ARG;
+    if (!c || !c->backend || n <= 0 || reps < 1 || mode < 0 || mode > 9) return RT_ERR_ARG;
     Backend* b = be(c);
     HIPCHK(c, hipSetDevice(b->device));
     if (c->dirty) {
@@ -2466,7 +2379,6 @@ extern "C" int rt_device_queries(rt_context* c, int mode, const float* rays, int
     const int threads = 256, blocks = std::min((n + threads - 1) / threads, cus * 8);
     const int qblocks = std::min((4 * n + threads - 1) / threads, cus * 16);
     const int rblocks = std::min((16 * n + threads - 1) / threads, cus * 16);
-    const int wblocks = std::min((64 * n + threads - 1) / threads, cus * 16);
     float4_* d_rays = nullptr;
     float* d_t = nullptr;
     int* d_k = nullptr;
@@ -2490,9 +2402,7 @@ extern "C" int rt_device_queries(rt_context* c, int mode, const float* rays, int
             case 6: hipLaunchKernelGGL((k_query_quad<false, 8>), dim3(qblocks), dim3(threads), 0, 0, b->view, d_rays, d_t, d_k, n); break;
             case 7: hipLaunchKernelGGL((k_query_quad<true, 8>), dim3(qblocks), dim3(threads), 0, 0, b->view, d_rays, d_t, d_k, n); break;
             case 8: hipLaunchKernelGGL((k_query_row<false>), dim3(rblocks), dim3(threads), 0, 0, b->view, d_rays, d_t, d_k, n); break;
-            case 9: hipLaunchKernelGGL((k_query_row<true>), dim3(rblocks), dim3(threads), 0, 0, b->view, d_rays, d_t, d_k, n); break;
-            case 10: hipLaunchKernelGGL((k_query_coop<false>), dim3(wblocks), dim3(threads), 0, 0, b->view, d_rays, d_t, d_k, n); break;
-            default: hipLaunchKernelGGL((k_query_coop<true>), dim3(wblocks), dim3(threads), 0, 0, b->view, d_rays, d_t, d_k, n); break;
+            default: hipLaunchKernelGGL((k_query_row<true>), dim3(rblocks), dim3(threads), 0, 0, b->view, d_rays, d_t, d_k, n); break;
         }
     };
     launch();  // warm-up

@@ -1,8 +1,7 @@
-"""Row walks (rt_row.h: 16 lanes per query over the 16-wide search BVH) and wave walks
-(rt_coop.h: a wave's four rows on one query) against the quad walks (rt_quad.h) and the
-exact octree walk, on the dragon stand-in.
+"""Row walks (rt_row.h: 16 lanes per query over the 16-wide search BVH) against the
+quad walks (rt_quad.h) and the exact octree walk, on the dragon stand-in.
 
-The row and wave walks must give the rt_fast.h answer exactly: the same closest (t, k) or
+The row walk must give the rt_fast.h answer exactly: the same closest (t, k) or
 occluded flag, and the same "needs the exact walk" verdict (-2), for every ray —
 tie-prone rays of the reference-pinned fixture (tests/golden/rays_dragon.npz,
 answers of the reference's own BVH::intersect), rays leaving the surface in
@@ -66,11 +65,6 @@ def test_gpu_row_walks_match_quad_walks_and_octree():
         aq, _ = _queries(rk, 5, rays)    # occlusion, quad walk
         ar, _ = _queries(rk, 9, rays)    # occlusion, row walk
         np.testing.assert_array_equal(ar.view(np.uint32), aq.view(np.uint32), err_msg=f"{name}: occlusion")
-        tw, kw = _queries(rk, 10, rays)  # closest, the wave's four rows
-        np.testing.assert_array_equal(tw.view(np.uint32), tq.view(np.uint32), err_msg=f"{name}: wave closest t")
-        np.testing.assert_array_equal(kw, kq, err_msg=f"{name}: wave closest k")
-        aw, _ = _queries(rk, 11, rays)   # occlusion, the wave's four rows
-        np.testing.assert_array_equal(aw.view(np.uint32), aq.view(np.uint32), err_msg=f"{name}: wave occlusion")
         assert (tr > 0).any() and (ar == 1.0).any(), name
         seen_unoccluded = seen_unoccluded or bool((ar == 0.0).any())
         # the settled closest answers against the exact octree walk (BVH::intersect)

@@ -70,8 +70,7 @@ def main():
     res = {}
     names = {0: "closest/node-walk", 1: "any/node-walk", 2: "closest/item-walk", 3: "any/item-walk",
              4: "closest/quad-walk", 5: "any/quad-walk", 6: "closest/quad-walk@8w", 7: "any/quad-walk@8w",
-             8: "closest/row-walk (16 lanes, 16-wide BVH)", 9: "any/row-walk (16 lanes, 16-wide BVH)",
-             10: "closest/wave-walk (4 rows, rt_coop.h)", 11: "any/wave-walk (4 rows, rt_coop.h)"}
+             8: "closest/row-walk (16 lanes, 16-wide BVH)", 9: "any/row-walk (16 lanes, 16-wide BVH)"}
     for m in [int(x) for x in args.modes.split(",")]:
         t = np.zeros(args.n, dtype=np.float32)
         k = np.zeros(args.n, dtype=np.int32)
@@ -85,7 +84,7 @@ def main():
                 "fallback": fb, "hits": int((t > 0).sum())}
         print(json.dumps(line), flush=True)
     # agreement between walks
-    for a, b in ((0, 2), (1, 3), (0, 4), (1, 5), (0, 6), (1, 7), (4, 8), (5, 9), (4, 10), (5, 11)):
+    for a, b in ((0, 2), (1, 3), (0, 4), (1, 5), (0, 6), (1, 7), (4, 8), (5, 9)):
         if a in res and b in res:
             ta, ka = res[a]
             tb, kb = res[b]
@@ -96,7 +95,7 @@ def main():
     # closest vs the exact octree walk on a subset
     sub = np.arange(0, args.n, max(1, args.n // 20000))
     ex = rk.intersect(rays[sub][:, [0, 1, 2, 4, 5, 6]])
-    for m in (0, 2, 4, 8, 10):
+    for m in (0, 2, 4, 8):
         if m not in res:
             continue
         t, k = res[m]
