@@ -66,7 +66,7 @@ static int run_wave_host(rt_context* c, int w, int h, int spp, int bounces, cons
     rtk::WaveView W{};
     W.park_cap = 1 << 14;
     W.spec_cam = 1;
-    if (const char* e = getenv("RT_SPEC_CAM")) W.spec_cam = atoi(e) != 0;
+    if (const char* e = getenv("RT_SPEC_CAM")) W.spec_cam = std::max(0, std::min(2, atoi(e)));
     W.spill_lanes = 0;  // the host threads keep their own spill areas
     W.shards = 1;       // one segment per queue (plain atomics on the host)
     W.seg_cap = n;

@@ -1727,7 +1727,9 @@ int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounces, cons
     int heavy_calls = RT_HEAVY_CALLS;
     if (const char* e = getenv("RT_HEAVY")) heavy_calls = std::max(0, atoi(e));
     int spec_cam = 1;  // the next sample's camera ray traced ahead (rt_wave.h next_camera); RT_SPEC_CAM=0: off
-    if (const char* e = getenv("RT_SPEC_CAM")) spec_cam = atoi(e) != 0;
+    if (const char* e = getenv("RT_SPEC_CAM")) spec_cam = std::max(0, std::min(2, atoi(e)));  // (2: rt_wave.h next_camera)
+    int tail_spec_cam = 1;  // ... in the tail kernel too (RT_TAIL_SPEC_CAM=0: not there)
+    if (const char* e = getenv("RT_TAIL_SPEC_CAM")) tail_spec_cam = atoi(e) != 0;
     // k_tail paths per wave: a round waits for the slowest walk of the wave's ~3 P queries, so
     // fewer paths per wave move each chain faster. With the entry held at the same live count
     // (r03, P x RT_TAIL_ENTER = 3.5): P = 5 / 3 / 2 / 1 -> cfg2 886-893 / 892-896 / 897-901 /
@@ -1917,6 +1919,7 @@ int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounces, cons
                 // few paths left and none waits: the tail kernel finishes them all
                 HIPCHK(c, hipMemsetAsync(La.cnt + C_TK_TAIL, 0, 4, La.s));
                 const dim3 g(tail_blocks);
+                La.W.spec_cam = tail_spec_cam ? spec_cam : 0;  // (the lane's last launch)
                 if (SEQ)
                     hipLaunchKernelGGL((tail_rows ? k_tail<true, false, 16> : k_tail<true, false, 4>), g, dim3(threads), 0, La.s, La.W, par, stats);
                 else if (S)

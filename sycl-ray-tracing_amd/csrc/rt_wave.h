@@ -250,6 +250,7 @@ struct PathReg {
     uint32_t flags;
     int bounce, sample;
     Col thr, sc, fin;
+    int last_end;  // the pixel's previous sample: its last shaded bounce (-1: none, -2: no sample yet)
 };
 
 RT_HD void load_path(const WaveView& W, int p, PathReg& P)
@@ -264,6 +265,7 @@ RT_HD void load_path(const WaveView& W, int p, PathReg& P)
     P.thr = colof(c);
     P.sample = (int)rt_asuint(c.w);
     P.sc = colof(d);
+    P.last_end = (int)rt_asuint(d.w);
     P.fin = colof(e);
 }
 
@@ -273,7 +275,7 @@ RT_HD void store_path(const WaveView& W, int p, const PathReg& P, bool fin_chang
     W.p_ro[p] = f4(P.ro, rt_asfloat(P.rng.a));
     W.p_rd[p] = f4(P.rd, rt_asfloat(P.flags | ((uint32_t)P.bounce << RT_FLAG_BITS)));
     W.p_thr[p] = f4(P.thr, rt_asfloat((uint32_t)P.sample));
-    W.p_sc[p] = f4(P.sc, 0.0f);
+    W.p_sc[p] = f4(P.sc, rt_asfloat((uint32_t)P.last_end));
     if (fin_changed) W.p_fin[p] = f4(P.fin, 0.0f);
 }
 
@@ -304,6 +306,9 @@ RT_HD void camera_ray(const WaveView& W, int x, int y, Rng& rng, V3& o, V3& d)
 RT_HD void next_camera(const WaveView& W, int p, const PathReg& P, Emit& e, uint32_t& fl)
 {
     if (!W.spec_cam || P.sample + 1 >= W.spp) return;
+    // spec_cam 2: where the sample may go on (a continuation is cast), only at the bounce
+    // where the pixel's previous sample ended (the camera ray: bounce -1)
+    if (W.spec_cam == 2 && (fl & PF_CONT) && P.last_end != -2 && P.last_end != P.bounce - 1) return;
     int x, y;
     pix_xy(W.src, p, x, y);
     Rng r = P.rng;
@@ -419,6 +424,7 @@ RT_HD void path_init(const WaveView& W, int p, Emit& e)
     for (int i = 0; i < 10; i++) P.rng.next();
     P.fin = col(0.0f);
     P.sample = 0;
+    P.last_end = -2;
     e.mask = 0;
     e.heavy = false;
     e.active = start_sample(W, p, P, e);
@@ -746,6 +752,7 @@ RT_HD void path_step(const WaveView& W, int p, Emit& e, Stats* st)
     }
     if (end) {
         fin_changed = true;
+        P.last_end = (P.flags & PF_END) ? P.bounce : P.bounce - 1;  // (a missed continuation: the bounce before)
         P.fin = cadd(P.fin, P.sc);
         bool start = ++P.sample < W.spp;
         if (start && (fl0 & PF_CAM)) {  // the next sample, its camera ray traced ahead: its answer now
@@ -755,6 +762,7 @@ RT_HD void path_step(const WaveView& W, int p, Emit& e, Stats* st)
                 start = false;
             } else {  // (bounce 0 missed: the sky, and that sample is over too)
                 if (W.bounces >= 2) P.sc = cadd(P.sc, cmul(env_from_dir(W.S, P.rd, st), P.thr));
+                P.last_end = -1;
                 P.fin = cadd(P.fin, P.sc);
                 start = ++P.sample < W.spp;
             }

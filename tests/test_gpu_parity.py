@@ -314,9 +314,10 @@ def test_gpu_schedules_bit_identical(monkeypatch):
         got = render(lanes, tail, enter=enter)
         np.testing.assert_array_equal(got.view(np.uint32), base.view(np.uint32),
                                       err_msg=f"lanes={lanes} tail={tail} enter={enter}")
-    for lanes, tail in ((1, 0), (3, 2)):
-        got = render(lanes, tail, spec_cam=0)
-        np.testing.assert_array_equal(got.view(np.uint32), base.view(np.uint32), err_msg=f"spec_cam=0 lanes={lanes}")
+    for lanes, tail, spec_cam in ((1, 0, 0), (3, 2, 0), (1, 0, 2), (3, 1, 2)):
+        got = render(lanes, tail, spec_cam=spec_cam)
+        np.testing.assert_array_equal(got.view(np.uint32), base.view(np.uint32),
+                                      err_msg=f"spec_cam={spec_cam} lanes={lanes}")
     # the walks by quads or by rows (rt_row.h) in the tail kernel, and rows in every k_trace launch
     # (and a k_trace drain continuing its quad walks as rows, or not; 1 walk at most, or 4)
     for rows, row_below, tail, enter, drain in ((0, 0, 2, 2.0, 0), (1, 0, 1, 1000.0, 1), (1, 1 << 30, 1, 2.0, 4),

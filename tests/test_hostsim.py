@@ -25,6 +25,18 @@ def test_hostsim_render_bit_exact(name, manifest, cameras):
     assert gio.compare_rgb(got, e["expected"])["bitwise_fraction"] == 1.0
 
 
+@pytest.mark.parametrize("spec_cam", [0, 2])
+def test_hostsim_camera_ahead_policies_bit_exact(spec_cam, manifest, cameras, monkeypatch):
+    """The next sample's camera ray traced ahead never (0) or only where the pixel's
+    previous sample ended (2, rt_wave.h next_camera): which rays are cast changes, the
+    answers do not."""
+    monkeypatch.setenv("RT_SPEC_CAM", str(spec_cam))
+    for name in rt_cases.CORNELL_CASES[:2]:
+        e = rt_cases.golden_case(name, manifest)
+        got = rt_cases.run_case(e, cameras, hostsim=True)
+        assert gio.compare_rgb(got, e["expected"])["bitwise_fraction"] == 1.0, name
+
+
 @pytest.mark.slow
 @pytest.mark.parametrize("name", ["cfg2_dragon", "cfg4_dragon4k", "cfg5_sweep_m0_r0", "cfg5_sweep_m3_r3"])
 def test_hostsim_dragon_bit_exact(name, manifest, cameras):

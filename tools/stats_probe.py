@@ -1,17 +1,49 @@
-"""One cfg2 render with the device counters on (rt_set_stats): the counts and the k_trace byte model split by record kind."""
-import sys, os, json
-sys.path.insert(0, 'sycl-ray-tracing_amd'); sys.path.insert(0, 'tools'); sys.path.insert(0, '.')
-import bench, rt_amd
-P, sky, cam17 = bench.build_inputs("cfg2")
-_, _, _, W, H, spp, nb, _ = bench.CONFIGS["cfg2"]
-rk = rt_amd.RenderKernel(W, H, spp, nb, rt_amd.Image(W, H), P.triangles, P.materials, P.emissive_triangle_indices,
-                         P.material_indices, None, rt_amd.BVH(P.triangles), rt_amd.Image.from_rgb(sky), None, device=0)
-rk.set_camera(rt_amd.Camera(cam17[:16], cam17[16]))
-rk.set_stats(True)
-rk.render()
-st = rk.stats()
-st = {k: int(v) for k, v in st.items()}
-b = bench.BYTES
-parts = {"box": b["box"] * (st.get("vol", 0) + st.get("any_vol", 0)), "tri": b["tri"] * (st.get("tri", 0) + st.get("any_tri", 0)),
-         "verify": b["verify"] * st.get("verify", 0), "ray": b["ray"] * (st.get("rays", 0) + st.get("any_rays", 0))}
-print(json.dumps({"stats": st, "bytes": parts}))
+"""Counters of one render (rt_set_stats): how the k_trace quad slots split between the
+streams and their drains, walk visits, fallbacks, path steps. One GPU.
+
+  python tools/stats_probe.py [--config cfg2] [--world 1]   (world > 1: rank 0's rows of that split)
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (os.path.join(REPO, "sycl-ray-tracing_amd"), os.path.join(REPO, "tools"), REPO):
+    sys.path.insert(0, p)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="cfg2")
+    ap.add_argument("--world", type=int, default=1)
+    args = ap.parse_args()
+    import torch
+    import bench
+    import rt_amd
+    from rt_amd.dist import ShardedFrame
+    scene, sky_kind, cam, W, H, spp, nb, desc = bench.CONFIGS[args.config]
+    P, sky, cam17 = bench.build_inputs(args.config)
+    rk = rt_amd.RenderKernel(W, H, spp, nb, rt_amd.Image(1, 1), P.triangles, P.materials,
+                             P.emissive_triangle_indices, P.material_indices, None, rt_amd.BVH(P.triangles),
+                             rt_amd.Image.from_rgb(sky), None, device=0)
+    rk.set_camera(rt_amd.Camera(cam17[:16], cam17[16]))
+    dev = torch.device("cuda", 0)
+    fr = ShardedFrame(rk, 0, args.world, device=dev)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    rk.set_stats(True)
+    fr.render(stream)
+    torch.cuda.synchronize(dev)
+    s = rk.stats()
+    rk.set_stats(False)
+    out = {"config": args.config, "world": args.world, "counters": s,
+           "drain_slot_fraction": round(s["drain_slots"] / max(1, s["wave_slots"] + s["drain_slots"]), 4),
+           "simt_stream": round((s["quad_visits"]) / max(1, s["wave_slots"]), 4),
+           "simt_drain": round(s["drain_visits"] / max(1, s["drain_slots"]), 4)}
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
