@@ -1728,8 +1728,15 @@ int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounces, cons
     if (const char* e = getenv("RT_HEAVY")) heavy_calls = std::max(0, atoi(e));
     int spec_cam = 1;  // the next sample's camera ray traced ahead (rt_wave.h next_camera); RT_SPEC_CAM=0: off
     if (const char* e = getenv("RT_SPEC_CAM")) spec_cam = std::max(0, std::min(2, atoi(e)));  // (2: rt_wave.h next_camera)
-    int tail_spec_cam = 1;  // ... in the tail kernel too (RT_TAIL_SPEC_CAM=0: not there)
-    if (const char* e = getenv("RT_TAIL_SPEC_CAM")) tail_spec_cam = atoi(e) != 0;
+    // The camera ray traced ahead costs a walk whenever the sample goes on. In k_tail a round
+    // waits for its path's slowest query, often that camera walk: there it is off (cfg4 8-way
+    // shard 352.3-354.6 -> 343.5 ms, cfg2 142.5-143.6 -> 141.3-141.6, profiles/r04q_cam.json).
+    int tail_spec_cam = 0;  // RT_TAIL_SPEC_CAM: the tail kernel's mode (0 / 1 / 2 as RT_SPEC_CAM)
+    if (const char* e = getenv("RT_TAIL_SPEC_CAM")) tail_spec_cam = std::max(0, std::min(2, atoi(e)));
+    // Above this many live paths in a lane (the throughput-bound launches) mode 2: a camera
+    // ray ahead only where the pixel's previous sample ended (fewer wasted walks, longer chains)
+    long spec_dense = 0;  // RT_SPEC_CAM_DENSE (0: off)
+    if (const char* e = getenv("RT_SPEC_CAM_DENSE")) spec_dense = std::max(0l, atol(e));
     // k_tail paths per wave: a round waits for the slowest walk of the wave's ~3 P queries, so
     // fewer paths per wave move each chain faster. With the entry held at the same live count
     // (r03, P x RT_TAIL_ENTER = 3.5): P = 5 / 3 / 2 / 1 -> cfg2 886-893 / 892-896 / 897-901 /
@@ -1877,6 +1884,7 @@ int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounces, cons
     };
     auto launch_step = [&](WaveLane& La) -> int {
         const int par = La.it & 1;
+        La.W.spec_cam = (spec_cam && spec_dense > 0 && La.live > spec_dense) ? 2 : spec_cam;
         if (S)
             hipLaunchKernelGGL(k_step<true>, dim3(step_blocks_of(La)), dim3(threads), 0, La.s, La.W, par, stats);
         else
@@ -1919,7 +1927,7 @@ int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounces, cons
                 // few paths left and none waits: the tail kernel finishes them all
                 HIPCHK(c, hipMemsetAsync(La.cnt + C_TK_TAIL, 0, 4, La.s));
                 const dim3 g(tail_blocks);
-                La.W.spec_cam = tail_spec_cam ? spec_cam : 0;  // (the lane's last launch)
+                La.W.spec_cam = spec_cam ? tail_spec_cam : 0;  // (the lane's last launch)
                 if (SEQ)
                     hipLaunchKernelGGL((tail_rows ? k_tail<true, false, 16> : k_tail<true, false, 4>), g, dim3(threads), 0, La.s, La.W, par, stats);
                 else if (S)
