@@ -1737,6 +1737,8 @@ int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounces, cons
     // ray ahead only where the pixel's previous sample ended (fewer wasted walks, longer chains)
     long spec_dense = 0;  // RT_SPEC_CAM_DENSE (0: off)
     if (const char* e = getenv("RT_SPEC_CAM_DENSE")) spec_dense = std::max(0l, atol(e));
+    long spec_sparse = 0;  // RT_SPEC_CAM_SPARSE: below this many live paths in a lane, none ahead (0: off)
+    if (const char* e = getenv("RT_SPEC_CAM_SPARSE")) spec_sparse = std::max(0l, atol(e));
     // k_tail paths per wave: a round waits for the slowest walk of the wave's ~3 P queries, so
     // fewer paths per wave move each chain faster. With the entry held at the same live count
     // (r03, P x RT_TAIL_ENTER = 3.5): P = 5 / 3 / 2 / 1 -> cfg2 886-893 / 892-896 / 897-901 /
@@ -1884,7 +1886,8 @@ int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounces, cons
     };
     auto launch_step = [&](WaveLane& La) -> int {
         const int par = La.it & 1;
-        La.W.spec_cam = (spec_cam && spec_dense > 0 && La.live > spec_dense) ? 2 : spec_cam;
+        La.W.spec_cam = (spec_cam && spec_dense > 0 && La.live > spec_dense) ? 2
+                        : (La.live < spec_sparse) ? 0 : spec_cam;
         if (S)
             hipLaunchKernelGGL(k_step<true>, dim3(step_blocks_of(La)), dim3(threads), 0, La.s, La.W, par, stats);
         else

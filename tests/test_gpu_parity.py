@@ -277,9 +277,10 @@ def test_gpu_schedules_bit_identical(monkeypatch):
     W, H, spp, nb = 640, 480, 2, 8
 
     def render(lanes, tail, off=0, stride=1, heavy=6, enter=2.0, spec_cam=1, rows=1, row_below=0, drain=4,
-               tail_cam=0, dense=0):
+               tail_cam=0, dense=0, sparse=0):
         monkeypatch.setenv("RT_TAIL_SPEC_CAM", str(tail_cam))
         monkeypatch.setenv("RT_SPEC_CAM_DENSE", str(dense))
+        monkeypatch.setenv("RT_SPEC_CAM_SPARSE", str(sparse))
         monkeypatch.setenv("RT_DRAIN_ROWS", str(drain))
         monkeypatch.setenv("RT_TAIL_ROWS", str(rows))
         monkeypatch.setenv("RT_ROW_BELOW", str(row_below))
@@ -319,11 +320,14 @@ def test_gpu_schedules_bit_identical(monkeypatch):
                                       err_msg=f"lanes={lanes} tail={tail} enter={enter}")
     # camera rays traced ahead: never, only where the pixel's previous sample ended (2), mode 2
     # in launches above a live count, and the tail kernel's own mode
-    for lanes, tail, spec_cam, tail_cam, dense in ((1, 0, 0, 0, 0), (3, 2, 0, 0, 0), (1, 0, 2, 0, 0), (3, 1, 2, 2, 0),
-                                                   (3, 1, 1, 1, 0), (3, 1, 1, 2, 0), (2, 1, 1, 0, 50000)):
-        got = render(lanes, tail, spec_cam=spec_cam, tail_cam=tail_cam, dense=dense)
+    for lanes, tail, spec_cam, tail_cam, dense, sparse in ((1, 0, 0, 0, 0, 0), (3, 2, 0, 0, 0, 0), (1, 0, 2, 0, 0, 0),
+                                                           (3, 1, 2, 2, 0, 0), (3, 1, 1, 1, 0, 0), (3, 1, 1, 2, 0, 0),
+                                                           (2, 1, 1, 0, 50000, 0), (2, 0, 1, 0, 0, 60000),
+                                                           (3, 1, 1, 1, 120000, 30000)):
+        got = render(lanes, tail, spec_cam=spec_cam, tail_cam=tail_cam, dense=dense, sparse=sparse)
         np.testing.assert_array_equal(got.view(np.uint32), base.view(np.uint32),
-                                      err_msg=f"spec_cam={spec_cam} tail_cam={tail_cam} dense={dense} lanes={lanes}")
+                                      err_msg=f"spec_cam={spec_cam} tail_cam={tail_cam} dense={dense} "
+                                              f"sparse={sparse} lanes={lanes}")
     # the walks by quads or by rows (rt_row.h) in the tail kernel, and rows in every k_trace launch
     # (and a k_trace drain continuing its quad walks as rows, or not; 1 walk at most, or 4)
     for rows, row_below, tail, enter, drain in ((0, 0, 2, 2.0, 0), (1, 0, 1, 1000.0, 1), (1, 1 << 30, 1, 2.0, 4),
