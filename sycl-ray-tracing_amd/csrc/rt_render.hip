@@ -164,12 +164,6 @@ struct Backend {
     DevBuf iterq;     // stats renders: per-iteration {queries, live slots} (RT_ITER_LOG)
     DevBuf wave[RT_MAX_LANES];      // per lane: path state, pending records, results, queues, lists
     DevBuf counters[RT_MAX_LANES];  // per lane: C_COUNT int32
-    // fast lane (RT_FAST_K): per lane its list + ticket, counters, samples-done histogram, spill
-    // area, stream (created on first use) and start / end events
-    DevBuf fast[RT_MAX_LANES], fcnt[RT_MAX_LANES], fhist[RT_MAX_LANES], fspill[RT_MAX_LANES];
-    int32_t* h_hist[RT_MAX_LANES] = {};
-    hipStream_t fs[RT_MAX_LANES] = {};
-    hipEvent_t fev_a[RT_MAX_LANES] = {}, fev_b[RT_MAX_LANES] = {};
     DevBuf xy;        // pixel list (rt_render_pixels)
     DevBuf fb;        // host-fb staging
     int32_t* h_act[RT_MAX_LANES] = {};     // per lane, pinned: live-slot counters (sharded) + 8 fallback counters
@@ -766,35 +760,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_STEP_OCC
         if (idx < n) {
             const int sh = shard_find(s_pre, RT_QSHARDS, idx);
             p = W.act_in[(size_t)sh * W.seg_cap + (idx - s_pre[sh])];
-            bool handed = false;
-            if (W.fast_cap > 0 && (int)rt_asuint(W.p_thr[p].w) <= W.fast_thr && W.r_park[p] == 0) {
-                const int j = atomicAdd(W.fast_ticket, 1);  // (to the fast lane: stepped there, not here)
-                if (j < W.fast_cap) {
-                    W.fast_list[j] = p;
-                    handed = true;
-                }
-            }
-            if (handed)
-                p = -1;
-            else
-                rtk::path_step(W, p, e, ps);
+            rtk::path_step(W, p, e, ps);
         }
         append_emit(W, par ^ 1, base, n, p, e);
     }
     flush_stats<STATS>(st, stats);
-}
-
-// Samples done by the live paths of iteration par's list (the fast lane's selection, run_wave).
-__global__ __launch_bounds__(256) void k_hist(rtk::WaveView W, int par, int32_t* __restrict__ hist)
-{
-    __shared__ int s_pre[RT_QSHARDS + 1];
-    shard_prefix(W.counters, RT_QSHARDS, [&](int j) { return ac_at(par, j); }, s_pre);
-    const int n = s_pre[RT_QSHARDS];
-    for (int idx = (int)(blockIdx.x * blockDim.x + threadIdx.x); idx < n; idx += (int)(gridDim.x * blockDim.x)) {
-        const int sh = shard_find(s_pre, RT_QSHARDS, idx);
-        const int p = W.act_in[(size_t)sh * W.seg_cap + (idx - s_pre[sh])];
-        atomicAdd(hist + min((int)rt_asuint(W.p_thr[p].w), W.spp), 1);
-    }
 }
 
 // A row's stack held in its wave's quad stacks (k_trace's drain, trace_stream): row k of a
@@ -1137,7 +1107,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TAIL_OCC
     rtk::lds_shade_init(W.S);  // (the env-map row search and a small material table from LDS)
     int32_t* cnt = W.counters;
     shard_prefix(cnt, RT_QSHARDS, [&](int j) { return ac_at(par, j); }, s_pre);
-    const int n = W.fast_cap > 0 ? min(s_pre[RT_QSHARDS], W.fast_cap) : s_pre[RT_QSHARDS];  // (fast lane: its list)
+    const int n = s_pre[RT_QSHARDS];
     const RtSceneView S = W.S;
     rtk::Stats st;
     if (STATS)
@@ -1542,14 +1512,8 @@ void destroy_one(Backend* b)
     for (DevBuf* d : all)
         if (d->p) (void)hipFree(d->p);
     for (int l = 0; l < RT_MAX_LANES; l++)
-        for (DevBuf* d : {&b->wave[l], &b->counters[l], &b->fast[l], &b->fcnt[l], &b->fhist[l], &b->fspill[l]})
+        for (DevBuf* d : {&b->wave[l], &b->counters[l]})
             if (d->p) (void)hipFree(d->p);
-    for (int l = 0; l < RT_MAX_LANES; l++) {
-        if (b->h_hist[l]) (void)hipHostFree(b->h_hist[l]);
-        if (b->fs[l]) (void)hipStreamDestroy(b->fs[l]);
-        if (b->fev_a[l]) (void)hipEventDestroy(b->fev_a[l]);
-        if (b->fev_b[l]) (void)hipEventDestroy(b->fev_b[l]);
-    }
     for (int l = 0; l < RT_MAX_LANES; l++) {
         if (b->h_act[l]) (void)hipHostFree(b->h_act[l]);
         if (b->ev_lane[l]) (void)hipEventDestroy(b->ev_lane[l]);
@@ -1725,8 +1689,6 @@ struct WaveLane {
     bool done = false, tail_next = false;
     int await = 0;  // 0 none, 1 live count, 2 fallback counts (tail entry check)
     hipEvent_t (*tev)[RT_MAX_TIMED_ITERS] = nullptr;  // [3][RT_MAX_TIMED_ITERS]
-    bool fast_pending = false, fast_sel = false;  // fast lane: selection due at the next k_step / done
-    int fast_thr = 0;
 };
 
 // Runs the wavefront loop for n slots of `src` into fb (device, n float4).
@@ -1777,14 +1739,6 @@ int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounces, cons
     // ray ahead only where the pixel's previous sample ended (fewer wasted walks, longer chains)
     long spec_dense = 0;  // RT_SPEC_CAM_DENSE (0: off)
     if (const char* e = getenv("RT_SPEC_CAM_DENSE")) spec_dense = std::max(0l, atol(e));
-    // Fast lane: once a lane's live paths fall below fast_at of its pixels, its fast_k paths with
-    // the fewest samples done (the pixels with the longest chains) leave the wavefront for a tail
-    // kernel on a stream of their own, stepping at a tail round's pace while the wavefront runs
-    // the rest (tools/fastlane_model.py). Off unless RT_FAST_K > 0.
-    int fast_k = 0;
-    if (const char* e = getenv("RT_FAST_K")) fast_k = std::max(0, std::min(1 << 16, atoi(e)));
-    double fast_at = 0.25;
-    if (const char* e = getenv("RT_FAST_AT")) fast_at = atof(e);
     int prio = 0;  // RT_PRIO: s_setprio 2 for k_tail (bit 0) and k_trace drains (bit 1)
     if (const char* e = getenv("RT_PRIO")) prio = atoi(e) & 3;
     long spec_sparse = 0;  // RT_SPEC_CAM_SPARSE: below this many live paths in a lane, none ahead (0: off)
@@ -1881,20 +1835,6 @@ int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounces, cons
         W.prio = prio;
         W.force_fb = force_fb;
         W.iterq = (S && iter_log && l == 0) ? (int32_t*)b->iterq.p : nullptr;
-        W.fast_cap = 0;
-        La.fast_pending = La.fast_sel = false;
-        if (fast_k > 0) {  // the fast lane's buffers, stream and events (first use)
-            const int fblocks = (fast_k + 3) / 4;  // (one path per wave)
-            if (int r = ensure(c, b->fast[l], (size_t)(fast_k + 1) * 4)) return r;
-            if (int r = ensure(c, b->fcnt[l], C_COUNT * sizeof(int32_t))) return r;
-            if (int r = ensure(c, b->fhist[l], (size_t)(spp + 1) * 4)) return r;
-            if (int r = ensure(c, b->fspill[l], (size_t)fblocks * threads * RT_STACK_CAP * 8)) return r;
-            if (!b->h_hist[l]) HIPCHK(c, hipHostMalloc((void**)&b->h_hist[l], (size_t)(1024 + 1) * 4, hipHostMallocDefault));
-            if (!b->fs[l]) HIPCHK(c, hipStreamCreateWithFlags(&b->fs[l], hipStreamNonBlocking));
-            if (!b->fev_a[l]) HIPCHK(c, hipEventCreateWithFlags(&b->fev_a[l], hipEventDisableTiming));
-            if (!b->fev_b[l]) HIPCHK(c, hipEventCreateWithFlags(&b->fev_b[l], hipEventDisableTiming));
-            HIPCHK(c, hipMemsetAsync(b->fcnt[l].p, 0, C_COUNT * sizeof(int32_t), La.s));
-        }
         La.lists[0] = (int32_t*)W.act_in;
         La.lists[1] = W.act_out;
         HIPCHK(c, hipMemsetAsync(La.cnt, 0, C_COUNT * sizeof(int32_t), La.s));
@@ -1953,47 +1893,10 @@ int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounces, cons
         const int par = La.it & 1;
         La.W.spec_cam = (spec_cam && spec_dense > 0 && La.live > spec_dense) ? 2
                         : (La.live < spec_sparse) ? 0 : spec_cam;
-        const int l = (int)(&La - L);
-        if (La.fast_pending) {  // this step hands the lane's slowest paths to the fast lane
-            int32_t* fl = (int32_t*)b->fast[l].p;
-            HIPCHK(c, hipMemsetAsync(fl + fast_k, 0, 4, La.s));
-            La.W.fast_list = fl;
-            La.W.fast_ticket = fl + fast_k;
-            La.W.fast_cap = fast_k;
-            La.W.fast_thr = La.fast_thr;
-        }
         if (S)
             hipLaunchKernelGGL(k_step<true>, dim3(step_blocks_of(La)), dim3(threads), 0, La.s, La.W, par, stats);
         else
             hipLaunchKernelGGL(k_step<false>, dim3(step_blocks_of(La)), dim3(threads), 0, La.s, La.W, par, stats);
-        if (La.fast_pending) {
-            La.W.fast_cap = 0;
-            La.fast_pending = false;
-            La.fast_sel = true;
-            // its tail kernel: the handed-over list as shard 0 of its own counters, its own spill
-            // area, a stream of its own (it runs beside the lane's next launches)
-            int32_t* fl = (int32_t*)b->fast[l].p;
-            int32_t* fc = (int32_t*)b->fcnt[l].p;
-            HIPCHK(c, hipMemcpyAsync(fc + ac_at(0, 0), fl + fast_k, 4, hipMemcpyDeviceToDevice, La.s));
-            HIPCHK(c, hipEventRecord(b->fev_a[l], La.s));
-            HIPCHK(c, hipStreamWaitEvent(b->fs[l], b->fev_a[l], 0));
-            rtk::WaveView FW = La.W;
-            FW.act_in = fl;
-            FW.counters = fc;
-            FW.fast_cap = fast_k;
-            FW.tail_paths = 1;  // (one path per wave, its queries on the wave's rows)
-            FW.spill_r = (uint32_t*)b->fspill[l].p;
-            FW.spill_k = (float*)((uint32_t*)b->fspill[l].p + (size_t)((fast_k + 3) / 4) * threads * RT_STACK_CAP);
-            FW.iterq = nullptr;
-            FW.spec_cam = spec_cam ? tail_spec_cam : 0;
-            const dim3 g((fast_k + 3) / 4);
-            if (S)
-                hipLaunchKernelGGL((k_tail<true, true, 16>), g, dim3(threads), 0, b->fs[l], FW, 0, stats);
-            else
-                hipLaunchKernelGGL((k_tail<false, true, 16>), g, dim3(threads), 0, b->fs[l], FW, 0, stats);
-            HIPCHK(c, hipGetLastError());
-            HIPCHK(c, hipEventRecord(b->fev_b[l], b->fs[l]));
-        }
         if (b->timing && La.it < RT_MAX_TIMED_ITERS) HIPCHK(c, hipEventRecord(La.tev[2][La.it], La.s));
         HIPCHK(c, hipGetLastError());
         La.it++;
@@ -2054,29 +1957,6 @@ int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounces, cons
         La.live = live;
         La.done = live == 0;
         La.tail_next = !La.done && live <= tail_max;
-        if (fast_k > 0 && tail_rows && !La.fast_sel && !La.done && !La.tail_next && spp <= 1024 &&
-            live < (long)(fast_at * La.n)) {
-            // the fast lane's threshold: the samples-done count of the fast_k-th slowest live path
-            const int l = (int)(&La - L);
-            int32_t* hh = (int32_t*)b->fhist[l].p;
-            HIPCHK(c, hipMemsetAsync(hh, 0, (size_t)(spp + 1) * 4, La.s));
-            rtk::WaveView HW = La.W;
-            HW.act_in = La.lists[La.it & 1];
-            hipLaunchKernelGGL(k_hist, dim3((unsigned)std::min(1024l, (live + threads - 1) / threads)), dim3(threads), 0,
-                               La.s, HW, La.it & 1, hh);
-            HIPCHK(c, hipGetLastError());
-            HIPCHK(c, hipMemcpyAsync(b->h_hist[l], hh, (size_t)(spp + 1) * 4, hipMemcpyDeviceToHost, La.s));
-            HIPCHK(c, hipStreamSynchronize(La.s));
-            long acc = 0;
-            int thr = spp;
-            for (int k = 0; k <= spp; k++)
-                if ((acc += b->h_hist[l][k]) >= fast_k) {
-                    thr = k;
-                    break;
-                }
-            La.fast_thr = thr;
-            La.fast_pending = true;
-        }
         return RT_OK;
     };
     for (int l = 0; l < nl; l++)
@@ -2113,7 +1993,6 @@ int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounces, cons
         if (!moved) std::this_thread::yield();
     }
     for (int l = 0; l < nl; l++) {  // each lane's pixels tone-mapped after its last step
-        if (L[l].fast_sel) HIPCHK(c, hipStreamWaitEvent(L[l].s, b->fev_b[l], 0));  // (and its fast lane's)
         hipLaunchKernelGGL(k_tonemap, dim3((L[l].n + threads - 1) / threads), dim3(threads), 0, L[l].s, L[l].W);
         HIPCHK(c, hipGetLastError());
     }

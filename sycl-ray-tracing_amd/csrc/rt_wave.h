@@ -123,11 +123,6 @@ struct WaveView {
     int32_t* iterq;         // stats renders: [iteration][2] = {queries, live slots} (else null)
     int iter;               // iteration of this launch
     int tail_paths;         // k_tail: paths per wave
-    // fast lane (run_wave RT_FAST_K): one k_step hands the live paths with at most fast_thr
-    // samples done (up to fast_cap of them) to a tail kernel on a stream of their own
-    int32_t* fast_list;     // the handed-over slots
-    int32_t* fast_ticket;   // their count (may pass fast_cap: the kernel clamps)
-    int fast_cap, fast_thr; // fast_cap 0: off (k_tail: the list's length cap)
     int drain_rows;         // k_trace: a wave's drain continues its walks as rows when at most this many remain
     int prio;               // issue priority (s_setprio) of latency-bound waves: bit 0 k_tail, bit 1 k_trace drains
     int force_fb;           // test knob (RT_FORCE_FALLBACK): a query whose ray hashes to 0 mod force_fb

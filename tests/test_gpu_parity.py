@@ -277,9 +277,7 @@ def test_gpu_schedules_bit_identical(monkeypatch):
     W, H, spp, nb = 640, 480, 2, 8
 
     def render(lanes, tail, off=0, stride=1, heavy=6, enter=2.0, spec_cam=1, rows=1, row_below=0, drain=4,
-               tail_cam=0, dense=0, sparse=0, fast_k=0, fast_at=0.25):
-        monkeypatch.setenv("RT_FAST_K", str(fast_k))
-        monkeypatch.setenv("RT_FAST_AT", str(fast_at))
+               tail_cam=0, dense=0, sparse=0):
         monkeypatch.setenv("RT_TAIL_SPEC_CAM", str(tail_cam))
         monkeypatch.setenv("RT_SPEC_CAM_DENSE", str(dense))
         monkeypatch.setenv("RT_SPEC_CAM_SPARSE", str(sparse))
@@ -330,12 +328,6 @@ def test_gpu_schedules_bit_identical(monkeypatch):
         np.testing.assert_array_equal(got.view(np.uint32), base.view(np.uint32),
                                       err_msg=f"spec_cam={spec_cam} tail_cam={tail_cam} dense={dense} "
                                               f"sparse={sparse} lanes={lanes}")
-    # the fast lane: a lane's slowest paths handed to a tail kernel on a stream of their own
-    # (a few, or most of the lane), the rest still in the wavefront
-    for lanes, tail, fast_k, fast_at in ((1, 1, 64, 0.95), (3, 1, 512, 0.95), (2, 1, 4096, 0.99), (3, 0, 256, 0.95)):
-        got = render(lanes, tail, fast_k=fast_k, fast_at=fast_at)
-        np.testing.assert_array_equal(got.view(np.uint32), base.view(np.uint32),
-                                      err_msg=f"fast_k={fast_k} fast_at={fast_at} lanes={lanes} tail={tail}")
     # the walks by quads or by rows (rt_row.h) in the tail kernel, and rows in every k_trace launch
     # (and a k_trace drain continuing its quad walks as rows, or not; 1 walk at most, or 4)
     for rows, row_below, tail, enter, drain in ((0, 0, 2, 2.0, 0), (1, 0, 1, 1000.0, 1), (1, 1 << 30, 1, 2.0, 4),
