@@ -873,7 +873,6 @@ __device__ __forceinline__ void trace_stream(const rtk::WaveView& W, const RtSce
             }
             cursor += __popcll(bidle);
             exhausted = (wg + (cursor >> 4) * wn) * 16 >= total;
-            if (exhausted && (W.prio & 2)) __builtin_amdgcn_s_setprio(2);  // (the drain: the launch's end)
             if (STATS && lane == 0) ps->c[RT_STAT_REFILLS]++;
         }
         const unsigned long long bact = __ballot(active && sub == 0);
@@ -1131,7 +1130,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TAIL_OCC
     long long tk_solo = 0;               // (RT_ITER_LOG: ... in walk trips with one group walking)
     int trips = 0, solo_trips = 0;
     const bool probe = STATS && W.iterq && W.iter + 1 < RT_MAX_TIMED_ITERS;
-    if (W.prio & 1) __builtin_amdgcn_s_setprio(2);  // (its rounds are the frame's last chains)
     for (;;) {
         // refill the wave's pool from the live list
         const bool need = lane < P && my < 0;
@@ -1739,8 +1737,6 @@ int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounces, cons
     // ray ahead only where the pixel's previous sample ended (fewer wasted walks, longer chains)
     long spec_dense = 0;  // RT_SPEC_CAM_DENSE (0: off)
     if (const char* e = getenv("RT_SPEC_CAM_DENSE")) spec_dense = std::max(0l, atol(e));
-    int prio = 0;  // RT_PRIO: s_setprio 2 for k_tail (bit 0) and k_trace drains (bit 1)
-    if (const char* e = getenv("RT_PRIO")) prio = atoi(e) & 3;
     long spec_sparse = 0;  // RT_SPEC_CAM_SPARSE: below this many live paths in a lane, none ahead (0: off)
     if (const char* e = getenv("RT_SPEC_CAM_SPARSE")) spec_sparse = std::max(0l, atol(e));
     // k_tail paths per wave: a round waits for the slowest walk of the wave's ~3 P queries, so
@@ -1832,7 +1828,6 @@ int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounces, cons
         W.counters = La.cnt;
         W.tail_paths = tail_p;
         W.drain_rows = drain_rows;
-        W.prio = prio;
         W.force_fb = force_fb;
         W.iterq = (S && iter_log && l == 0) ? (int32_t*)b->iterq.p : nullptr;
         La.lists[0] = (int32_t*)W.act_in;

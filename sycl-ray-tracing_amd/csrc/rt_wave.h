@@ -124,7 +124,6 @@ struct WaveView {
     int iter;               // iteration of this launch
     int tail_paths;         // k_tail: paths per wave
     int drain_rows;         // k_trace: a wave's drain continues its walks as rows when at most this many remain
-    int prio;               // issue priority (s_setprio) of latency-bound waves: bit 0 k_tail, bit 1 k_trace drains
     int force_fb;           // test knob (RT_FORCE_FALLBACK): a query whose ray hashes to 0 mod force_fb
                             // skips the quad walk and takes the exact octree walk (0: off)
     int shards, seg_cap;    // queues and live lists: `shards` segments of seg_cap entries (device: rt_render.hip)
