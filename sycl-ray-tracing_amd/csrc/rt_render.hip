@@ -1067,9 +1067,7 @@ __device__ __noinline__ int tail_step(const rtk::WaveView& W, int my, int last_k
     if (my >= 0) rtk::path_step(W, my, e, ps);
     int nl[2];
     tail_lists(e, my, last_kind, l0, l1, nl);
-    // (bit 30: a camera ray ahead and no continuation: the sample ends at the next step for certain)
-    const bool cam_certain = my >= 0 && ((e.mask >> rtk::RK_CAM) & 1u) && !((e.mask >> rtk::RK_CONT) & 1u);
-    return (e.active ? 1 : 0) | (nl[0] << 1) | (nl[1] << 11) | (cam_certain ? 1 << 30 : 0);
+    return (e.active ? 1 : 0) | (nl[0] << 1) | (nl[1] << 11);
 }
 // k_tail's inline exact walk (a query the quad walk cannot settle: ~1e-6 of them), kept
 // out of line so that its registers do not add to the tail loop's: inlined, k_tail
@@ -1132,13 +1130,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TAIL_OCC
     long long tk_solo = 0;               // (RT_ITER_LOG: ... in walk trips with one group walking)
     int trips = 0, solo_trips = 0;
     const bool probe = STATS && W.iterq && W.iter + 1 < RT_MAX_TIMED_ITERS;
-    // a group's walk; with cam_async a camera ray traced ahead may go on walking across a step
-    const bool cam_async = G == 16 && P == 1 && W.cam_async;
-    bool act = false;
-    int l = 0;
-    uint32_t target = 0;
-    rtk::QState q;
-    bool cam_certain = false;
     for (;;) {
         // refill the wave's pool from the live list
         const bool need = lane < P && my < 0;
@@ -1155,8 +1146,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TAIL_OCC
                 my = W.act_in[(size_t)sh * W.seg_cap + (idx - s_pre[sh])];
             }
         }
-        // (a camera walk still running here is one the step will not read: dropped, unwritten)
-        act = false;
         if (!__any(my >= 0)) break;
         rounds++;
         // step; the emitted rays -> the wave's LDS lists
@@ -1166,8 +1155,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TAIL_OCC
             const int r = tail_step(W, my, last_kind, s_q[wv][0], s_q[wv][1], ps);
             if (!(r & 1)) my = -1;
             nl[0] = (r >> 1) & 0x3ff;
-            nl[1] = (r >> 11) & 0x3ff;
-            cam_certain = __ballot(((r >> 30) & 1) != 0) != 0;
+            nl[1] = r >> 11;
         }
         long long t1 = 0;
         if (probe) {
@@ -1182,7 +1170,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TAIL_OCC
         // the slowest of every 16-query pass
         const int nq = nl[0] + nl[1];
         int next = 0;  // the next query of the lists (uniform)
-        bool cont_missed = false;  // (cam_async: this round's continuation missed, or took the exact walk)
+        bool act = false;
+        int l = 0;
+        uint32_t target = 0;
+        rtk::QState q;
         for (;;) {
             bool exact = false;
             const unsigned long long bidle = __ballot(!act && sub == 0);
@@ -1204,7 +1195,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TAIL_OCC
                             else
                                 rtk::finish_any(W, target, false);
                         }
-                        if (!act && l == 0 && (target & 7u) == (uint32_t)rtk::RK_CONT) cont_missed = true;
                     }
                 }
                 next = min(nq, next + __popcll(bidle));
@@ -1236,10 +1226,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TAIL_OCC
                             rtk::finish_any(W, target, q.h.k == 1);
                     }
                     exact = !ok;
-                    if (l == 0 && (target & 7u) == (uint32_t)rtk::RK_CONT && (!ok || !(t > 0.0f))) cont_missed = true;
                 }
             }
-            if (exact && l == 0 && (target & 7u) == (uint32_t)rtk::RK_CONT) cont_missed = true;
             if (exact && sub == 0) {  // the exact octree walk, to completion
                 if (STATS) st.c[RT_STAT_FALLBACK]++;
                 xs.f = stk;
@@ -1253,16 +1241,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TAIL_OCC
                     tk_solo += __shfl(te, 0) - __shfl(ts, 0);
                 }
             }
-            if (next >= nq) {
-                if (!cam_async) {
-                    if (!__any(act)) break;
-                } else {
-                    // done when only a camera walk is left whose answer the next step will not read
-                    const bool is_cam = l == 0 && (target & 7u) == (uint32_t)rtk::RK_CAM;
-                    const bool need_cam = cam_certain || __ballot(cont_missed) != 0;
-                    if (!__any(act && (!is_cam || need_cam))) break;
-                }
-            }
+            if (next >= nq && !__any(act)) break;
         }
         if (probe) {
             const long long t2 = wall_clock64();
@@ -1754,8 +1733,6 @@ int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounces, cons
     // shard 352.3-354.6 -> 343.5 ms, cfg2 142.5-143.6 -> 141.3-141.6, profiles/r04q_cam.json).
     int tail_spec_cam = 0;  // RT_TAIL_SPEC_CAM: the tail kernel's mode (0 / 1 / 2 as RT_SPEC_CAM)
     if (const char* e = getenv("RT_TAIL_SPEC_CAM")) tail_spec_cam = std::max(0, std::min(2, atoi(e)));
-    int tail_cam_async = 0;  // RT_TAIL_CAM_ASYNC: a tail round does not wait for a camera walk it will not read
-    if (const char* e = getenv("RT_TAIL_CAM_ASYNC")) tail_cam_async = atoi(e) != 0;
     // Above this many live paths in a lane (the throughput-bound launches) mode 2: a camera
     // ray ahead only where the pixel's previous sample ended (fewer wasted walks, longer chains)
     long spec_dense = 0;  // RT_SPEC_CAM_DENSE (0: off)
@@ -1851,7 +1828,6 @@ int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounces, cons
         W.counters = La.cnt;
         W.tail_paths = tail_p;
         W.drain_rows = drain_rows;
-        W.cam_async = 0;
         W.force_fb = force_fb;
         W.iterq = (S && iter_log && l == 0) ? (int32_t*)b->iterq.p : nullptr;
         La.lists[0] = (int32_t*)W.act_in;
@@ -1955,7 +1931,6 @@ int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounces, cons
                 HIPCHK(c, hipMemsetAsync(La.cnt + C_TK_TAIL, 0, 4, La.s));
                 const dim3 g(tail_blocks);
                 La.W.spec_cam = spec_cam ? tail_spec_cam : 0;  // (the lane's last launch)
-                La.W.cam_async = tail_cam_async;
                 if (SEQ)
                     hipLaunchKernelGGL((tail_rows ? k_tail<true, false, 16> : k_tail<true, false, 4>), g, dim3(threads), 0, La.s, La.W, par, stats);
                 else if (S)

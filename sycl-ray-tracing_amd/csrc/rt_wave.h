@@ -123,8 +123,6 @@ struct WaveView {
     int32_t* iterq;         // stats renders: [iteration][2] = {queries, live slots} (else null)
     int iter;               // iteration of this launch
     int tail_paths;         // k_tail: paths per wave
-    int cam_async;          // k_tail (one path per wave, rows): a camera ray traced ahead does not hold up the
-                            // round; the next step waits for it only if it needs its answer
     int drain_rows;         // k_trace: a wave's drain continues its walks as rows when at most this many remain
     int force_fb;           // test knob (RT_FORCE_FALLBACK): a query whose ray hashes to 0 mod force_fb
                             // skips the quad walk and takes the exact octree walk (0: off)

@@ -277,8 +277,7 @@ def test_gpu_schedules_bit_identical(monkeypatch):
     W, H, spp, nb = 640, 480, 2, 8
 
     def render(lanes, tail, off=0, stride=1, heavy=6, enter=2.0, spec_cam=1, rows=1, row_below=0, drain=4,
-               tail_cam=0, dense=0, sparse=0, cam_async=0):
-        monkeypatch.setenv("RT_TAIL_CAM_ASYNC", str(cam_async))
+               tail_cam=0, dense=0, sparse=0):
         monkeypatch.setenv("RT_TAIL_SPEC_CAM", str(tail_cam))
         monkeypatch.setenv("RT_SPEC_CAM_DENSE", str(dense))
         monkeypatch.setenv("RT_SPEC_CAM_SPARSE", str(sparse))
@@ -329,12 +328,6 @@ def test_gpu_schedules_bit_identical(monkeypatch):
         np.testing.assert_array_equal(got.view(np.uint32), base.view(np.uint32),
                                       err_msg=f"spec_cam={spec_cam} tail_cam={tail_cam} dense={dense} "
                                               f"sparse={sparse} lanes={lanes}")
-    # camera rays ahead in the tail kernel whose walks a round waits for only when the next step
-    # reads them (tail kernel entered at once and at the default point)
-    for lanes, tail, tail_cam, enter in ((3, 1, 1, 1000.0), (2, 1, 2, 1000.0), (3, 1, 1, 2.0)):
-        got = render(lanes, tail, tail_cam=tail_cam, enter=enter, cam_async=1)
-        np.testing.assert_array_equal(got.view(np.uint32), base.view(np.uint32),
-                                      err_msg=f"cam_async tail_cam={tail_cam} lanes={lanes} enter={enter}")
     # the walks by quads or by rows (rt_row.h) in the tail kernel, and rows in every k_trace launch
     # (and a k_trace drain continuing its quad walks as rows, or not; 1 walk at most, or 4)
     for rows, row_below, tail, enter, drain in ((0, 0, 2, 2.0, 0), (1, 0, 1, 1000.0, 1), (1, 1 << 30, 1, 2.0, 4),
