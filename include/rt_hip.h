@@ -68,6 +68,27 @@ int rt_device_count(const rt_context* ctx);
  * per-device error slots. Never called by the product paths. */
 int rt_create_multi_loopback(int n_devices, const int* devices, rt_context** out);
 int rt_test_fail_device(rt_context* ctx, int device);
+/* TEST ONLY. rt_test_schedule: override one wavefront-schedule parameter of
+ * ctx's later renders (keys: "lanes", "tail_paths" (0: no tail kernel),
+ * "tail_enter", "tail_rows", "drain_rows", "heavy_calls", "spec_cam",
+ * "tail_spec_cam", "step_budget", the stressor "force_fallback" (every k-th
+ * query by a ray hash skips to the exact octree walk), "reset"). No parameter
+ * changes a result; the product never calls it and reads no schedule from the
+ * environment. RT_ERR_ARG for an unknown key. */
+int rt_test_schedule(rt_context* ctx, const char* key, double value);
+/* TEST ONLY. Walk log of stats renders (rt_set_stats): every search-BVH walk of
+ * at least min_calls quad_visit calls (a row trip counts 2) is recorded, up to
+ * capacity records (min_calls 0: off); sample_every > 1 keeps only the walks
+ * whose (path slot, iteration, kind) hash is 0 modulo it. A record is RT_WLOG_FLOATS floats:
+ * origin xyz, kind | where << 8 (int bits; where 0 k_trace quads, 1 a k_trace
+ * drain's rows, 2 k_tail), direction xyz, calls (int bits), t (closest: the
+ * answer, -1 none, -2 left to the exact walk; occlusion: 1 occluded / 0 not),
+ * triangle (int bits), iteration (int bits), path slot (int bits).
+ * rt_test_walk_log_read copies up to capacity records of the last stats render
+ * and returns how many walks qualified (>= the records copied). */
+#define RT_WLOG_FLOATS 12
+int rt_test_walk_log(rt_context* ctx, int min_calls, int sample_every, int capacity);
+long rt_test_walk_log_read(const rt_context* ctx, float* out, long capacity);
 void rt_destroy(rt_context* ctx);
 const char* rt_last_error(const rt_context* ctx); /* ctx may be NULL: last global error */
 int rt_version(void);
@@ -178,6 +199,10 @@ int rt_read_hdr(const char* path, int flip_y, int* width, int* height, float* pi
  * flip_y, written as a PNG. rt_image_to_rgba8 is the conversion alone. */
 int rt_write_png(const char* path, const float* rgba, int width, int height, int flip_y);
 int rt_image_to_rgba8(const float* rgba, long n_pixels, unsigned char* out);
+/* TEST ONLY. rt_mesh_load parses files of at least `bytes` in chunks on worker
+ * threads (-1: the default, 4 MB; 0: every file, so small test files take the
+ * chunked path). */
+int rt_test_obj_parallel_min(long bytes);
 /* Octree of a triangle buffer without a device (parity tests). */
 long rt_octree_dump(const float* triangles, int n_triangles, int max_depth, int leaf_max, void* buf, long capacity);
 

@@ -21,6 +21,13 @@ void set_global_err(const std::string& m)
 
 void rt_err_sink(std::string* sink) { tl_sink = sink; }
 
+void rt_read_diag(rt_context* c)
+{
+    if (const char* e = std::getenv("RT_TIMELINE")) c->diag.timeline = e;
+    if (const char* e = std::getenv("RT_ITER_LOG")) c->diag.iter_log = e;
+    c->diag.verbose = std::getenv("RT_VERBOSE") != nullptr;
+}
+
 int rt_fail(rt_context* ctx, int code, const std::string& msg)
 {
     if (tl_sink) {  // a device thread of a multi-device render: its own slot (rt_for_devices)
@@ -63,6 +70,8 @@ RtSceneView rt_host_view(const rt_context* c)
     v.chain_monotone = c->flat.chain_monotone ? 1 : 0;
     v.bvh4 = c->flat.bvh4.data();
     v.bvh16 = c->flat.bvh16.data();
+    v.bvh4s = c->flat.bvh4s.data();
+    v.bvh16s = c->flat.bvh16s.data();
     v.bvh_tri4 = c->flat.bvh_tri4.data();
     v.parent = c->flat.parent.data();
     v.leaf_of = c->flat.leaf_of.data();
@@ -100,6 +109,7 @@ int rt_create(int device, rt_context** out)
     *out = nullptr;
     rt_context* c = new rt_context();
     c->device = device;
+    rt_read_diag(c);
     int r = rt_backend_create(c);
     if (r) {
         set_global_err(c->err);
@@ -134,6 +144,7 @@ int create_multi(int n_devices, const int* devices, bool loopback, rt_context** 
     for (int d = 0; d < n_devices; d++) c->devices.push_back(devices ? devices[d] : d);
     c->device = c->devices[0];
     c->loopback = loopback;
+    rt_read_diag(c);
     int r = rt_backend_create(c);
     if (r) {
         set_global_err(c->err);
@@ -162,6 +173,53 @@ int rt_test_fail_device(rt_context* c, int device)
     if (!c) return rt_fail(nullptr, RT_ERR_ARG, "rt_test_fail_device: ctx is NULL");
     c->fail_device = device;
     return RT_OK;
+}
+
+int rt_test_schedule(rt_context* c, const char* key, double value)
+{
+    if (!c || !key) return rt_fail(c, RT_ERR_ARG, "rt_test_schedule: ctx or key is NULL");
+    RtSchedule& s = c->sched;
+    const std::string k = key;
+    const int v = (int)value;
+    if (k == "lanes") s.lanes = std::max(0, v);
+    else if (k == "tail_paths") s.tail_paths = v;
+    else if (k == "tail_enter") s.tail_enter = value;
+    else if (k == "tail_rows") s.tail_rows = v;
+    else if (k == "drain_rows") s.drain_rows = std::min(4, v);
+    else if (k == "heavy_calls") s.heavy_calls = v;
+    else if (k == "spec_cam") s.spec_cam = std::min(2, v);
+    else if (k == "tail_spec_cam") s.tail_spec_cam = std::min(2, v);
+    else if (k == "force_fallback") s.force_fallback = std::max(0, v);
+    else if (k == "step_budget") s.step_budget = v;
+    else if (k == "reset") s = RtSchedule{};
+    else return rt_fail(c, RT_ERR_ARG, "rt_test_schedule: unknown key " + k);
+    return RT_OK;
+}
+
+int rt_test_obj_parallel_min(long bytes)
+{
+    rt::g_obj_parallel_min.store(bytes < 0 ? -1 : bytes);
+    return RT_OK;
+}
+
+int rt_test_walk_log(rt_context* c, int min_calls, int sample_every, int capacity)
+{
+    if (!c || min_calls < 0 || capacity < 0) return rt_fail(c, RT_ERR_ARG, "rt_test_walk_log: bad arguments");
+    c->diag.wlog_min = min_calls;
+    c->diag.wlog_every = std::max(1, sample_every);
+    c->diag.wlog_cap = min_calls > 0 ? capacity : 0;
+    c->diag.wlog.clear();
+    c->diag.wlog_total = 0;
+    return RT_OK;
+}
+
+long rt_test_walk_log_read(const rt_context* c, float* out, long capacity)
+{
+    if (!c || capacity < 0 || (capacity > 0 && !out)) return rt_fail(nullptr, RT_ERR_ARG, "rt_test_walk_log_read: bad arguments");
+    const long n = (long)(c->diag.wlog.size() / RT_WLOG_FLOATS);
+    const long m = std::min(n, capacity);
+    if (m > 0) std::memcpy(out, c->diag.wlog.data(), (size_t)m * RT_WLOG_FLOATS * sizeof(float));
+    return c->diag.wlog_total;
 }
 
 int rt_device_count(const rt_context* ctx) { return ctx ? (ctx->devices.empty() ? 1 : (int)ctx->devices.size()) : RT_ERR_ARG; }

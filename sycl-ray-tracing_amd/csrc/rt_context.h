@@ -14,8 +14,41 @@
 #include "rt_device.h"
 #include "rt_scene.h"
 
+// Schedule of the wavefront loop (rt_render.hip run_wave). The product runs the defaults
+// (-1: the backend's own choice); rt_test_schedule (tests and measurement tools only,
+// include/rt_hip.h) overrides them per context. No parameter changes a pixel: the GPU
+// schedule tests render with each and compare the bits. Nothing here is read from the
+// environment.
+struct RtSchedule {
+    int lanes = 0;             // wavefront lanes per render (0: auto, rt_device_set_lanes)
+    int tail_paths = -1;       // k_tail paths per wave (0: no tail kernel)
+    double tail_enter = -1.0;  // k_tail entry: live paths per lane, in grid-fills' pools
+    int tail_rows = -1;        // k_tail walks by rows (1) or quads (0)
+    int drain_rows = -1;       // k_trace: a drain's last walks continue as rows (0: off)
+    int heavy_calls = -1;      // k_trace heavy class threshold in quad_visit calls (0: off)
+    int spec_cam = -1;         // camera ray traced ahead: 0 never, 1 always, 2 where the last sample ended
+    int tail_spec_cam = -1;    // the same in k_tail
+    int force_fallback = 0;    // stressor: every k-th query (by a ray hash) skips to the exact walk
+    int step_budget = -1;      // exact-walk steps per query per launch before it parks
+};
+
+// Diagnostics, read from the environment once when the context is created (rt_create*):
+// RT_TIMELINE (per-launch timeline file), RT_ITER_LOG (per-iteration log prefix),
+// RT_VERBOSE. They change no result and no schedule.
+struct RtDiag {
+    std::string timeline, iter_log;
+    bool verbose = false;
+    // walk log (rt_test_walk_log): stats renders record every search-BVH walk of at least
+    // min_calls quad_visit calls (row trips count 2), up to cap records of RT_WLOG_FLOATS
+    int wlog_min = 0, wlog_cap = 0, wlog_every = 1;
+    std::vector<float> wlog;  // the last stats render's records
+    long wlog_total = 0;      // walks that qualified (may exceed cap)
+};
+
 struct rt_context {
     int device = 0;
+    RtSchedule sched;
+    RtDiag diag;
     // rt_create_multi: the devices a render shards over (rows y -> device y mod N, RCCL
     // scatter / gather through devices[0]); empty for a single-device context (rt_create).
     // One entry: a single-device context on that ordinal (nothing to shard, no RCCL)
@@ -74,6 +107,8 @@ int rt_backend_render_pixels(rt_context* ctx, int w, int h, int spp, int bounces
 int rt_backend_intersect(rt_context* ctx, const float* rays, int n, void* out);
 
 int rt_fail(rt_context* ctx, int code, const std::string& msg);
+// RtDiag from the environment (rt_create*)
+void rt_read_diag(rt_context* ctx);
 // While set (per host thread), rt_fail writes its message to *sink instead of the
 // context: the per-device threads of a multi-device render report into their own
 // slots, and the caller raises the error once, after the join (rt_for_devices).

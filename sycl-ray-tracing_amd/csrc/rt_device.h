@@ -104,6 +104,8 @@ struct RtSceneView {
     // search BVH + octree back-links for the verification walk
     const Bvh4Node* bvh4;      // [0] = root
     const Bvh4Child* bvh16;    // 16-wide form, RT_BVH16_W records per node, node 0 = root
+    const float4_* bvh4s;      // oriented slab of each 4-wide child ([node * 4 + c]; rt_fast.h slab_ok)
+    const float4_* bvh16s;     // the same, in bvh16's record order ([node * RT_BVH16_W + j])
     const float4_* bvh_tri4;   // 3 records per triangle in BVH leaf order: {a.xyz, k}, {e1, leaf record}, {e2}
     const int32_t* parent;     // octree record -> parent record (-1 for the root)
     const int32_t* leaf_of;    // leaf-order triangle k -> its octree leaf record

@@ -72,6 +72,61 @@ RT_HD bool box_hit(const float* mn, const float* mx, const RayB& r, float tmax, 
     return t0 <= t1 && t1 >= 0.0f;
 }
 
+// Entry and exit distances of a box (box_hit's arithmetic) for the slab test below.
+RT_HD bool box_hit2(const float* mn, const float* mx, const RayB& r, float tmax, float& tnear, float& tfar)
+{
+    float t0 = -__builtin_inff(), t1 = tmax;
+#pragma unroll
+    for (int i = 0; i < 3; i++) {
+#if defined(__HIP_DEVICE_COMPILE__) && RT_BOX_FMA
+        const float a = __builtin_fmaf(mn[i], r.inv[i], r.oi[i]), b = __builtin_fmaf(mx[i], r.inv[i], r.oi[i]);
+#else
+        const float a = mn[i] * r.inv[i] + r.oi[i], b = mx[i] * r.inv[i] + r.oi[i];
+#endif
+        t0 = __builtin_fmaxf(t0, __builtin_fminf(a, b));
+        t1 = __builtin_fminf(t1, __builtin_fmaxf(a, b));
+    }
+    tnear = t0;
+    tfar = t1;
+    return t0 <= t1 && t1 >= 0.0f;
+}
+
+// f16 bits -> f32 (the slab normals: finite, |x| <= 1)
+RT_HD float rt_half(uint32_t h)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    return (float)__builtin_bit_cast(_Float16, (uint16_t)h);
+#else
+    const uint32_t e = (h >> 10) & 31u, m = h & 1023u;
+    const float mag = e == 0 ? (float)m * 0x1p-24f : (float)(1024u + m) * __builtin_ldexpf(1.0f, (int)e - 25);
+    return (h & 0x8000u) ? -mag : mag;
+#endif
+}
+
+// Oriented slab of a search-BVH child (rt_scene.cpp build_slabs): s = {normal x | y << 16 and
+// z as f16 bits, lo, hi}. The ray's segment [max(t0, 0), t1] inside the child's box can only
+// reach a triangle of the child if it meets {lo <= n.x <= hi}; false when the whole segment
+// lies on one side. Conservative: the host's margin covers this f32 arithmetic for any ray
+// inside the scene's box; a child without a slab has n = 0, lo = -inf, hi = +inf
+// (and a NaN from inf * 0 only drops that endpoint: fmin / fmax).
+#ifndef RT_SLABS
+#define RT_SLABS 1
+#endif
+RT_HD bool slab_ok(const float4_& s, V3 o, V3 d, float t0, float t1)
+{
+    const uint32_t w = rt_asuint(s.x);
+    const float nx = rt_half(w & 0xffffu), ny = rt_half(w >> 16), nz = rt_half(rt_asuint(s.y) & 0xffffu);
+#if defined(__HIP_DEVICE_COMPILE__)
+    const float no = __builtin_fmaf(nz, o.z, __builtin_fmaf(ny, o.y, nx * o.x));
+    const float nd = __builtin_fmaf(nz, d.z, __builtin_fmaf(ny, d.y, nx * d.x));
+    const float p0 = __builtin_fmaf(__builtin_fmaxf(t0, 0.0f), nd, no), p1 = __builtin_fmaf(t1, nd, no);
+#else
+    const float no = nx * o.x + ny * o.y + nz * o.z, nd = nx * d.x + ny * d.y + nz * d.z;
+    const float p0 = no + __builtin_fmaxf(t0, 0.0f) * nd, p1 = no + t1 * nd;
+#endif
+    return !(__builtin_fmaxf(p0, p1) < s.z || __builtin_fminf(p0, p1) > s.w);
+}
+
 struct Bvh4R {
     float lo[3][4], hi[3][4];
     int32_t ref[4], cnt[4];
@@ -100,12 +155,16 @@ RT_HD Bvh4R load_bvh4(const Bvh4Node* nodes, int i)
 }
 
 // The four child boxes of a node: entry distance and "passes within [0, tmax]".
-RT_HD void box4(const Bvh4R& n, const RayB& r, float tmax, float* tn, bool* hit)
+// (and their oriented slabs, slab_ok, when the scene has them: node's records S.bvh4s[4 node + c])
+RT_HD void box4(const RtSceneView& S, int node, const Bvh4R& n, const RayB& r, V3 o, V3 d, float tmax, float* tn,
+                bool* hit)
 {
 #pragma unroll
     for (int c = 0; c < 4; c++) {
         const float mn[3] = {n.lo[0][c], n.lo[1][c], n.lo[2][c]}, mx[3] = {n.hi[0][c], n.hi[1][c], n.hi[2][c]};
-        hit[c] = n.cnt[c] >= 0 && box_hit(mn, mx, r, tmax, tn[c]);
+        float tf;
+        hit[c] = n.cnt[c] >= 0 && box_hit2(mn, mx, r, tmax, tn[c], tf);
+        if (RT_SLABS && hit[c] && S.bvh4s) hit[c] = slab_ok(S.bvh4s[4 * (size_t)node + c], o, d, tn[c], tf);
     }
 }
 
@@ -235,7 +294,7 @@ RT_HD void fast_closest(const RtSceneView& S, V3 o, V3 d, STK& stk, FastHit& h, 
         if (st) st->c[RT_STAT_VOL] += 4;
         float tn[4];
         bool hit[4];
-        box4(n, rb, h.t + h.t * RT_T2_WINDOW, tn, hit);
+        box4(S, cur, n, rb, o, d, h.t + h.t * RT_T2_WINDOW, tn, hit);
 #pragma unroll
         for (int c = 0; c < 4; c++)
             if (hit[c] && n.cnt[c] > 0) fast_leaf(S, n.ref[c], n.cnt[c], o, d, h, st);
@@ -360,7 +419,7 @@ RT_HD void fast_closest_u(const RtSceneView& S, V3 o, V3 d, STK& stk, FastHit& h
             float tn[4];
             bool hit[4];
             const float tmax = h.t + h.t * RT_T2_WINDOW;
-            box4(n, rb, tmax, tn, hit);
+            box4(S, cur, n, rb, o, d, tmax, tn, hit);
             float k[4];
             int v[4];
             bool ok[4];
@@ -442,7 +501,7 @@ RT_HD int fast_any_u(const RtSceneView& S, V3 o, V3 d, STK& stk, Stats* st)
             if (st) st->c[RT_STAT_ANY_VOL] += 4;
             float tn[4];
             bool hit[4];
-            box4(n, rb, __builtin_inff(), tn, hit);
+            box4(S, cur, n, rb, o, d, __builtin_inff(), tn, hit);
             bool over = false;
 #pragma unroll
             for (int c = 0; c < 4; c++) {
@@ -531,7 +590,7 @@ RT_HD int fast_query_any(const RtSceneView& S, V3 o, V3 d, STK& stk, Stats* st)
         if (st) st->c[RT_STAT_ANY_VOL] += 4;
         float tn[4];
         bool hit[4];
-        box4(n, rb, __builtin_inff(), tn, hit);
+        box4(S, cur, n, rb, o, d, __builtin_inff(), tn, hit);
 #pragma unroll
         for (int c = 0; c < 4; c++) {
             if (!hit[c] || n.cnt[c] <= 0) continue;

@@ -65,8 +65,8 @@ static int run_wave_host(rt_context* c, int w, int h, int spp, int bounces, cons
     if (n <= 0) return RT_OK;
     rtk::WaveView W{};
     W.park_cap = 1 << 14;
-    W.spec_cam = 1;
-    if (const char* e = getenv("RT_SPEC_CAM")) W.spec_cam = std::max(0, std::min(2, atoi(e)));
+    W.spec_cam = c->sched.spec_cam >= 0 ? c->sched.spec_cam : 1;  // (rt_test_schedule; the product's default)
+    W.force_fb = c->sched.force_fallback;
     W.spill_lanes = 0;  // the host threads keep their own spill areas
     W.shards = 1;       // one segment per queue (plain atomics on the host)
     W.seg_cap = n;
@@ -203,7 +203,8 @@ static int run_wave_host(rt_context* c, int w, int h, int spp, int bounces, cons
                 rtk::RayRec r = rtk::queue_item(W, counters, rtk::RK_CONT, last_kind, idx, target);
                 float t;
                 int k;
-                if (rtk::fast_query_closest(W.S, rtk::v3of(r.o), rtk::v3of(r.d), fst, t, k, ps)) {
+                if (!rtk::forced_fallback(W.force_fb, r.o, r.d) &&
+                    rtk::fast_query_closest(W.S, rtk::v3of(r.o), rtk::v3of(r.d), fst, t, k, ps)) {
                     rtk::finish_closest(W, target, rtk::v3of(r.o), rtk::v3of(r.d), t, k);
                 } else {
                     r.d.w = rt_asfloat(target & 7u);
@@ -215,7 +216,8 @@ static int run_wave_host(rt_context* c, int w, int h, int spp, int bounces, cons
             for (int idx = 0; idx < nqa; idx++) {
                 uint32_t target;
                 rtk::RayRec r = rtk::queue_item(W, counters, rtk::RK_ESH, rtk::RK_BENV, idx, target);
-                const int a = rtk::fast_query_any(W.S, rtk::v3of(r.o), rtk::v3of(r.d), fst, ps);
+                const int a = rtk::forced_fallback(W.force_fb, r.o, r.d) ? -1
+                              : rtk::fast_query_any(W.S, rtk::v3of(r.o), rtk::v3of(r.d), fst, ps);
                 if (a >= 0) {
                     rtk::finish_any(W, target, a == 1);
                 } else {

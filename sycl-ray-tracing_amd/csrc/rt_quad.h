@@ -82,22 +82,39 @@ __device__ __forceinline__ void child_record(const RtSceneView& S, int node, int
     b = p[1];
 }
 
-// Lane `sub`'s child of inner node `node`: box test within [0, tmax].
+// Oriented slabs (rt_fast.h slab_ok) in the quad walks: each lane also loads its child's
+// 16-B slab record in the same round trip.
+#ifndef RT_SLAB_QUAD
+#define RT_SLAB_QUAD RT_SLABS
+#endif
+
+// Lane `sub`'s child of inner node `node`: box (and slab) test within [0, tmax].
 struct QChild {
     int item;  // node index or leaf item (rt_fast.h leaf_item)
     bool ok;
     float tn;
 };
-__device__ __forceinline__ QChild quad_child(const RtSceneView& S, int node, int sub, const RayB& rb, float tmax)
+__device__ __forceinline__ QChild quad_child(const RtSceneView& S, int node, int sub, const RayB& rb, float tmax, V3 o,
+                                             V3 d)
 {
     float4_ a, b;
     child_record(S, node, sub, a, b);
+#if RT_SLAB_QUAD
+    const float4_ sl = S.bvh4s[4 * (size_t)node + sub];
+    rt_pin(sl);
+#endif
     rt_pin(a);
     rt_pin(b);
     const int ref = (int)rt_asuint(b.z), cnt = (int)rt_asuint(b.w);
     const float mn[3] = {a.x, a.y, a.z}, mx[3] = {a.w, b.x, b.y};
     QChild c;
-    c.ok = cnt >= 0 && box_hit(mn, mx, rb, tmax, c.tn) && c.tn <= tmax;
+    float tf;
+    c.ok = cnt >= 0 && box_hit2(mn, mx, rb, tmax, c.tn, tf) && c.tn <= tmax;
+#if RT_SLAB_QUAD
+    c.ok = c.ok && slab_ok(sl, o, d, c.tn, tf);
+#else
+    (void)o, (void)d;
+#endif
     c.item = cnt > 0 ? leaf_item(ref, cnt) : ref;
     return c;
 }
@@ -264,15 +281,25 @@ __device__ __forceinline__ int quad_visit(const RtSceneView& S, QState& q, QSTK&
             }
             if (st && sub == 0) st->c[RT_STAT_ANY_VOL] += 4 * m;
             float4_ r0[NW], r1[NW];
+#if RT_SLAB_QUAD
+            float4_ sl[NW];
+#endif
 #pragma unroll
             for (int j = 0; j < NW; j++) {
                 r0[j] = r1[j] = float4_{0.0f, 0.0f, 0.0f, 0.0f};
+#if RT_SLAB_QUAD
+                sl[j] = float4_{0.0f, 0.0f, -__builtin_inff(), __builtin_inff()};
+                if (j < m) sl[j] = S.bvh4s[4 * (size_t)nd[j] + sub];
+#endif
                 if (j < m) child_record(S, nd[j], sub, r0[j], r1[j]);
             }
 #pragma unroll
             for (int j = 0; j < NW; j++) {
                 rt_pin(r0[j]);
                 rt_pin(r1[j]);
+#if RT_SLAB_QUAD
+                rt_pin(sl[j]);
+#endif
             }
             int base = 0, first = 0;
             bool any_first = false;
@@ -280,8 +307,13 @@ __device__ __forceinline__ int quad_visit(const RtSceneView& S, QState& q, QSTK&
             for (int j = 0; j < NW; j++) {
                 const int ref = (int)rt_asuint(r1[j].z), cnt = (int)rt_asuint(r1[j].w);
                 const float mn[3] = {r0[j].x, r0[j].y, r0[j].z}, mx[3] = {r0[j].w, r1[j].x, r1[j].y};
-                float tn;
-                const bool ok = j < m && cnt >= 0 && box_hit(mn, mx, q.rb, __builtin_inff(), tn);
+                float tn, tf;
+#if RT_SLAB_QUAD
+                const bool ok = j < m && cnt >= 0 && box_hit2(mn, mx, q.rb, __builtin_inff(), tn, tf) &&
+                                slab_ok(sl[j], q.o, q.d, tn, tf);
+#else
+                const bool ok = j < m && cnt >= 0 && box_hit2(mn, mx, q.rb, __builtin_inff(), tn, tf);
+#endif
                 const int item = cnt > 0 ? leaf_item(ref, cnt) : ref;
                 const int o = ok ? 1 : 0;
                 const int o1 = qdpp<RT_QX1>(o), o2 = qdpp<RT_QX2>(o), o3 = qdpp<RT_QX3>(o);
@@ -309,7 +341,7 @@ __device__ __forceinline__ int quad_visit(const RtSceneView& S, QState& q, QSTK&
         }
         if (st && sub == 0) st->c[RT_STAT_VOL] += 4;
         const float tmax = h.t + h.t * RT_T2_WINDOW;
-        const QChild c = quad_child(S, q.cur, sub, q.rb, tmax);
+        const QChild c = quad_child(S, q.cur, sub, q.rb, tmax, q.o, q.d);
         const float key = c.ok ? c.tn : __builtin_inff();
         // rank by (key, lane): the nearest hit child has rank 0
         const float k1 = qdppf<RT_QX1>(key), k2 = qdppf<RT_QX2>(key), k3 = qdppf<RT_QX3>(key);

@@ -53,9 +53,6 @@ namespace {
 #ifndef RT_STEP_OCC
 #define RT_STEP_OCC 3  // k_step waves per SIMD
 #endif
-#ifndef RT_ROW_BELOW
-#define RT_ROW_BELOW 0  // k_trace walks with rows (rt_row.h) below this many live paths per lane
-#endif
 #ifndef RT_TAIL_ROWS
 #define RT_TAIL_ROWS 1  // k_tail walks with rows (rt_row.h)
 #endif
@@ -159,9 +156,10 @@ struct Backend {
     int index = 0;    // position in the context's device list (0: the root)
     hipStream_t own = nullptr;  // device-side work not on a caller's stream (multi-device shards, pixel lists)
     DevBuf nodes, tri4, prim2k, mat_idx, mats, emissive, spheres, env, env_lum, cdf;
-    DevBuf bvh4, bvh16, bvh_tri4, parent, leaf_of, cdf_row, cdf_coarse, cdf_fence, matk;
+    DevBuf bvh4, bvh16, bvh4s, bvh16s, bvh_tri4, parent, leaf_of, cdf_row, cdf_coarse, cdf_fence, matk;
     DevBuf stats;     // 2 x RT_STAT_COUNT u64: all kernels, then the tail kernel's share
     DevBuf iterq;     // stats renders: per-iteration {queries, live slots} (RT_ITER_LOG)
+    DevBuf wlog;      // stats renders with a walk log: count (256 B), then 3 float4 per record
     DevBuf wave[RT_MAX_LANES];      // per lane: path state, pending records, results, queues, lists
     DevBuf counters[RT_MAX_LANES];  // per lane: C_COUNT int32
     DevBuf xy;        // pixel list (rt_render_pixels)
@@ -472,7 +470,7 @@ struct FastStack {
 // RT_FORCE_FALLBACK: does this query skip the quad walk (a schedule-independent hash of the ray)?
 __device__ __forceinline__ bool forced_fallback(const rtk::WaveView& W, const float4_& o, const float4_& d)
 {
-    return W.force_fb > 0 && ((rt_asuint(o.x) ^ rt_asuint(d.y) ^ (rt_asuint(d.z) >> 7)) % (uint32_t)W.force_fb) == 0u;
+    return rtk::forced_fallback(W.force_fb, o, d);
 }
 
 // Blocks [0, n0) take role 0, the rest role 1, in proportion to the work.
@@ -767,6 +765,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_STEP_OCC
     flush_stats<STATS>(st, stats);
 }
 
+// Stats renders with a walk log (rt_test_walk_log, include/rt_hip.h): one record per walk of at
+// least W.wlog_min quad_visit calls. where: 0 k_trace quads, 1 a k_trace drain's rows, 2 k_tail.
+__device__ __noinline__ void walk_log(const rtk::WaveView& W, rtk::V3 o, rtk::V3 d, uint32_t target, int calls, float t,
+                                      int k, int where)
+{
+    if (W.wlog_every > 1 && ((target * 2654435761u) ^ ((uint32_t)W.iter * 40503u)) % (uint32_t)W.wlog_every != 0u) return;
+    const int i = atomicAdd(W.wlog_n, 1);
+    if (i >= W.wlog_cap) return;
+    float4_* r = W.wlog + 3 * (size_t)i;
+    r[0] = float4_{o.x, o.y, o.z, rt_asfloat((target & 7u) | ((uint32_t)where << 8))};
+    r[1] = float4_{d.x, d.y, d.z, rt_asfloat((uint32_t)calls)};
+    r[2] = float4_{t, rt_asfloat((uint32_t)k), rt_asfloat((uint32_t)W.iter), rt_asfloat(target >> 3)};
+}
+
 // A row's stack held in its wave's quad stacks (k_trace's drain, trace_stream): row k of a
 // wave uses the words of the wave's quads 4k .. 4k+3, entry e at depth e >> 2 of quad
 // 4k + (e & 3), so converting the wave's walks to rows needs no other LDS.
@@ -815,8 +827,8 @@ __device__ __forceinline__ void trace_stream(const rtk::WaveView& W, const RtSce
     // a walk's end: its answer, or the exact walk's list; gs = lanes of the group walking it
     auto finish = [&](int res, int gs) {
         // a long walk: the path's next rays go to the heavy class (head of the next streams)
-        // (a row call covers two 4-wide levels: counted twice)
-        if (W.r_heavy && sub == 0 && (gs == 4 ? q.calls : 2 * q.calls) >= W.heavy_calls) W.r_heavy[target >> 3] = 1;
+        // (q.calls counts quad_visit calls; a row call covers two 4-wide levels and counts 2)
+        if (W.r_heavy && sub == 0 && q.calls >= W.heavy_calls) W.r_heavy[target >> 3] = 1;
         if (STATS && W.iterq && sub == 0 && W.iter < RT_MAX_TIMED_ITERS) {
             // (RT_ITER_LOG: the launch's longest walk in quad_visit calls per role, and
             // how many walks took more than 8)
@@ -829,6 +841,8 @@ __device__ __forceinline__ void trace_stream(const rtk::WaveView& W, const RtSce
         // (rows: each quad of the row verifies alike; one counts)
         if (res > 0 && !ANY && !rtk::quad_closest_answer(S, q, sub & 3, t, k, gs == 4 || sub == 0 ? ps : nullptr))
             res = -1;
+        if (STATS && W.wlog && sub == 0 && q.calls >= W.wlog_min)
+            walk_log(W, q.o, q.d, target, q.calls, res <= 0 ? -2.0f : ANY ? (float)(q.h.k == 1) : t, k, gs == 4 ? 0 : 1);
         if (sub == 0) {
             if (res > 0) {
                 if (ANY)
@@ -891,7 +905,7 @@ __device__ __forceinline__ void trace_stream(const rtk::WaveView& W, const RtSce
                 res = rtk::quad_visit<ANY, RT_VISIT_DESCEND, PAIR>(S, q, stk, sub, ps);
             else
                 res = rtk::row_visit<ANY, RT_VISIT_DESCEND>(S, q, stk, sub, ps);
-            q.calls++;
+            q.calls += G == 4 ? 1 : 2;
             if (res != 0) {
                 active = false;
                 finish(res, G);
@@ -942,7 +956,7 @@ __device__ __forceinline__ void trace_stream(const rtk::WaveView& W, const RtSce
             }
             if (active) {
                 const int res = rtk::row_visit<ANY, RT_VISIT_DESCEND>(S, q, rs, sub, ps);
-                q.calls++;
+                q.calls += 2;
                 if (res != 0) {
                     active = false;
                     finish(res, 16);
@@ -1189,6 +1203,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TAIL_OCC
                         exact = true;
                     } else {
                         act = l ? rtk::qstate_begin<true>(q, q.o, q.d, sub, ps) : rtk::qstate_begin<false>(q, q.o, q.d, sub, ps);
+                        if (STATS) q.calls = 0;
                         if (!act && sub == 0) {  // (a NaN ray: no hit)
                             if (l == 0)
                                 rtk::finish_closest(W, target, q.o, q.d, -1.0f, -1);
@@ -1213,12 +1228,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TAIL_OCC
                 else
                     res = l ? rtk::row_visit<true, RT_TAIL_DESCEND>(S, q, stk, sub, ps)
                             : rtk::row_visit<false, RT_TAIL_DESCEND>(S, q, stk, sub, ps);
+                if (STATS) q.calls += G == 4 ? 1 : 2;
                 if (res != 0) {
                     act = false;
                     float t = 0.0f;
                     int k = 0;
                     const bool ok = res > 0 && (l == 1 || rtk::quad_closest_answer(S, q, sub & 3, t, k,
                                                                                     G == 4 || sub == 0 ? ps : nullptr));
+                    if (STATS && W.wlog && sub == 0 && q.calls >= W.wlog_min)
+                        walk_log(W, q.o, q.d, target, q.calls, !ok ? -2.0f : l ? (float)(q.h.k == 1) : t, k, 2);
                     if (ok && sub == 0) {
                         if (l == 0)
                             rtk::finish_closest(W, target, q.o, q.d, t, k);
@@ -1495,8 +1513,6 @@ int create_one(rt_context* c, int device, Backend** out)
     HIPCHK(c, hipStreamCreateWithFlags(&b->own, hipStreamNonBlocking));
     HIPCHK(c, hipEventCreateWithFlags(&b->ev_fork, hipEventDisableTiming));
     HIPCHK(c, hipEventCreateWithFlags(&b->ev_done, hipEventDisableTiming));
-    if (const char* e = getenv("RT_LANES")) b->lanes = std::min(RT_MAX_LANES, std::max(1, atoi(e)));
-    if (const char* e = getenv("RT_STEP_BUDGET")) b->budget = std::max(1, atoi(e));
     return RT_OK;
 }
 
@@ -1505,8 +1521,8 @@ void destroy_one(Backend* b)
     (void)hipSetDevice(b->device);
     (void)hipDeviceSynchronize();
     DevBuf* all[] = {&b->nodes, &b->tri4, &b->prim2k, &b->mat_idx, &b->mats, &b->emissive, &b->spheres, &b->env,
-                     &b->env_lum, &b->cdf, &b->bvh4, &b->bvh16, &b->bvh_tri4, &b->parent, &b->leaf_of, &b->cdf_row, &b->cdf_coarse,
-                     &b->cdf_fence, &b->matk, &b->stats, &b->xy, &b->fb, &b->iterq};
+                     &b->env_lum, &b->cdf, &b->bvh4, &b->bvh16, &b->bvh4s, &b->bvh16s, &b->bvh_tri4, &b->parent, &b->leaf_of, &b->cdf_row, &b->cdf_coarse,
+                     &b->cdf_fence, &b->matk, &b->stats, &b->xy, &b->fb, &b->iterq, &b->wlog};
     for (DevBuf* d : all)
         if (d->p) (void)hipFree(d->p);
     for (int l = 0; l < RT_MAX_LANES; l++)
@@ -1554,6 +1570,7 @@ int upload_one(rt_context* c, Backend* b, const std::vector<int32_t>& matk, bool
         (r = upload(c, b->spheres, c->spheres)) || (r = upload(c, b->env, c->env)) ||
         (r = upload(c, b->env_lum, c->env_lum)) || (r = upload(c, b->cdf, c->cdf)) ||
         (r = upload(c, b->bvh4, c->flat.bvh4)) || (r = upload(c, b->bvh16, c->flat.bvh16)) ||
+        (r = upload(c, b->bvh4s, c->flat.bvh4s)) || (r = upload(c, b->bvh16s, c->flat.bvh16s)) ||
         (r = upload(c, b->bvh_tri4, c->flat.bvh_tri4)) ||
         (r = upload(c, b->parent, c->flat.parent)) || (r = upload(c, b->leaf_of, c->flat.leaf_of)) ||
         (r = upload(c, b->cdf_row, c->cdf_row)) || (r = upload(c, b->cdf_coarse, c->cdf_coarse)) ||
@@ -1589,6 +1606,8 @@ int upload_one(rt_context* c, Backend* b, const std::vector<int32_t>& matk, bool
     v.brute = c->brute ? 1 : 0;
     v.bvh4 = (const Bvh4Node*)b->bvh4.p;
     v.bvh16 = (const Bvh4Child*)b->bvh16.p;
+    v.bvh4s = (const float4_*)b->bvh4s.p;
+    v.bvh16s = (const float4_*)b->bvh16s.p;
     v.bvh_tri4 = (const float4_*)b->bvh_tri4.p;
     v.parent = (const int32_t*)b->parent.p;
     v.leaf_of = (const int32_t*)b->leaf_of.p;
@@ -1705,61 +1724,51 @@ int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounces, cons
     // k_trace grid-fills (RT_TRACE_FILLS): with per-wave query streams one fill is best, a wave's
     // stream is longer and its end (the last long walk) costs less; cfg2: 0.75 / 1 / 1.25 / 1.5 / 2 / 3
     // -> 739 / 730-740 / 731 / 724 / 708-710 / 692 Msamples/s
-    double trace_fills = 1.0;
-    if (const char* e = getenv("RT_TRACE_FILLS")) trace_fills = std::max(0.25, atof(e));
-    const int trace_blocks = (int)(dev_cus * trace_fills * RT_TRACE_OCC);
+    const int trace_blocks = dev_cus * RT_TRACE_OCC;
+    const RtSchedule& sc = c->sched;
+    const RtDiag& dg = c->diag;
     const bool S = c->stats_enabled;
     const bool SEQ = S && c->stats_seq;  // (counter renders with unpaired occlusion walks: rt_set_stats(ctx, 2))
     unsigned long long* stats = (unsigned long long*)b->stats.p;
     if (S) HIPCHK(c, hipMemsetAsync(b->stats.p, 0, b->stats.bytes, s));
-    const char* iter_log = getenv("RT_ITER_LOG");  // per-iteration log of lane 0: counts (stats renders) / ms (timed)
+    const char* iter_log = dg.iter_log.empty() ? nullptr : dg.iter_log.c_str();  // per-iteration log of lane 0: counts (stats renders) / ms (timed)
+    const bool wlog = S && dg.wlog_cap > 0 && b->index == 0;
+    if (wlog) {
+        if (int r = ensure(c, b->wlog, 256 + (size_t)dg.wlog_cap * 48)) return r;
+        HIPCHK(c, hipMemsetAsync(b->wlog.p, 0, 256, s));
+    }
     if (S && iter_log) {
         if (int r = ensure(c, b->iterq, RT_MAX_TIMED_ITERS * 24)) return r;
         HIPCHK(c, hipMemsetAsync(b->iterq.p, 0, RT_MAX_TIMED_ITERS * 24, s));
     }
     // lanes: rows interleave (row j of the launch -> lane j % lanes); pixel lists split in runs
-    int nl = b->lanes > 0 ? b->lanes : n <= RT_LANES4_MAX ? 4 : 3;
+    const int lanes_set = sc.lanes > 0 ? std::min(RT_MAX_LANES, sc.lanes) : b->lanes;
+    int nl = lanes_set > 0 ? lanes_set : n <= RT_LANES4_MAX ? 4 : 3;
     const int rows = src.xy ? 0 : n / src.W;
     while (nl > 1 && (n < nl * 65536 || (!src.xy && rows < nl))) nl--;
     WaveLane L[RT_MAX_LANES];
-    int force_fb = 0;
-    if (const char* e = getenv("RT_FORCE_FALLBACK")) force_fb = std::max(0, atoi(e));
-    int heavy_calls = RT_HEAVY_CALLS;
-    if (const char* e = getenv("RT_HEAVY")) heavy_calls = std::max(0, atoi(e));
-    int spec_cam = 1;  // the next sample's camera ray traced ahead (rt_wave.h next_camera); RT_SPEC_CAM=0: off
-    if (const char* e = getenv("RT_SPEC_CAM")) spec_cam = std::max(0, std::min(2, atoi(e)));  // (2: rt_wave.h next_camera)
+    const int force_fb = sc.force_fallback;  // (test stressor, rt_test_schedule)
+    const int heavy_calls = sc.heavy_calls >= 0 ? sc.heavy_calls : RT_HEAVY_CALLS;
+    // the next sample's camera ray traced ahead (rt_wave.h next_camera): 1; 0 off; 2 only where
+    // the pixel's previous sample ended (cfg2 -1.5 ms, the cfg4 8-way shard unchanged, r04)
+    const int spec_cam = sc.spec_cam >= 0 ? sc.spec_cam : 1;
     // The camera ray traced ahead costs a walk whenever the sample goes on. In k_tail a round
     // waits for its path's slowest query, often that camera walk: there it is off (cfg4 8-way
     // shard 352.3-354.6 -> 343.5 ms, cfg2 142.5-143.6 -> 141.3-141.6, profiles/r04q_cam.json).
-    int tail_spec_cam = 0;  // RT_TAIL_SPEC_CAM: the tail kernel's mode (0 / 1 / 2 as RT_SPEC_CAM)
-    if (const char* e = getenv("RT_TAIL_SPEC_CAM")) tail_spec_cam = std::max(0, std::min(2, atoi(e)));
-    // Above this many live paths in a lane (the throughput-bound launches) mode 2: a camera
-    // ray ahead only where the pixel's previous sample ended (fewer wasted walks, longer chains)
-    long spec_dense = 0;  // RT_SPEC_CAM_DENSE (0: off)
-    if (const char* e = getenv("RT_SPEC_CAM_DENSE")) spec_dense = std::max(0l, atol(e));
-    long spec_sparse = 0;  // RT_SPEC_CAM_SPARSE: below this many live paths in a lane, none ahead (0: off)
-    if (const char* e = getenv("RT_SPEC_CAM_SPARSE")) spec_sparse = std::max(0l, atol(e));
+    const int tail_spec_cam = sc.tail_spec_cam >= 0 ? sc.tail_spec_cam : 0;  // the tail kernel's mode (as spec_cam)
     // k_tail paths per wave: a round waits for the slowest walk of the wave's ~3 P queries, so
     // fewer paths per wave move each chain faster. With the entry held at the same live count
     // (r03, P x RT_TAIL_ENTER = 3.5): P = 5 / 3 / 2 / 1 -> cfg2 886-893 / 892-896 / 897-901 /
     // 887-890 Msamples/s, cfg4 8-way shard (slowest rank) 401 / - / 390 / 405 ms
     // row walks (rt_row.h, 16 lanes per query over the 16-wide BVH) where walks are latency-bound:
-    // the tail kernel (tail_rows, on: its rounds wait for their slowest walk), and k_trace launches
-    // of lanes with fewer than row_below live paths (off: a sparse launch still has more queries
-    // than rows, and a row walk's throughput is lower). cfg4 8-way shard, one MI355X
-    // (profiles/r04c_row_probe.json, r04d_tail_probe.json): quads 380-382 ms; tail rows 367-370;
-    // k_trace rows below 32 K / 131 K paths 415 / 420-428 ms.
-    long row_below = RT_ROW_BELOW;
-    if (const char* e = getenv("RT_ROW_BELOW")) row_below = atol(e);
-    int tail_rows = RT_TAIL_ROWS;
-    if (const char* e = getenv("RT_TAIL_ROWS")) tail_rows = atoi(e) != 0;
-    const bool host_blocking = getenv("RT_HOST_BLOCKING") && atoi(getenv("RT_HOST_BLOCKING")) != 0;  // (A/B: round 3's loop)
-    int drain_rows = RT_DRAIN_ROWS;  // k_trace: a drain's walks continue as rows (trace_stream)
-    if (const char* e = getenv("RT_DRAIN_ROWS")) drain_rows = std::max(0, std::min(4, atoi(e)));
+    // the tail kernel (tail_rows: its rounds wait for their slowest walk). cfg4 8-way shard, one
+    // MI355X (profiles/r04c_row_probe.json, r04d_tail_probe.json): quads 380-382 ms; tail rows
+    // 367-370; rows for whole k_trace launches below 32 K / 131 K paths 415 / 420-428 ms (removed).
+    const int tail_rows = sc.tail_rows >= 0 ? (sc.tail_rows != 0) : RT_TAIL_ROWS;
+    const int drain_rows = sc.drain_rows >= 0 ? sc.drain_rows : RT_DRAIN_ROWS;  // k_trace: a drain's walks continue as rows
     // (rows: one path per wave, its ~4 queries on the wave's 4 rows: shard 367 ms vs 2 / 3 paths
     // 373-378 / 373-375 at the same entry live count)
-    int tail_p = tail_rows ? 1 : 2;
-    if (const char* e = getenv("RT_TAIL_PATHS")) tail_p = std::min(RT_TAIL_MAXP, std::max(0, atoi(e)));
+    const int tail_p = sc.tail_paths >= 0 ? std::min(RT_TAIL_MAXP, sc.tail_paths) : tail_rows ? 1 : 2;
     const int tail_blocks = dev_cus * RT_TAIL_OCC;  // one grid-fill of k_tail
     // a lane enters the tail kernel at 2x one grid-fill's pool (the waves refill from the live
     // list): with 2 paths per wave, RT_TAIL_ENTER = 1.4 / 1.75 / 2.2 / 2.8 -> cfg2 888-897 /
@@ -1768,8 +1777,7 @@ int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounces, cons
     // (4 lanes, the auto count of launches of <= 1.5 M slots: 1.4 — cfg4 8-way shard, 4 rounds on
     // one MI355X: 2.0 / 1.5 / 1.25 / 1.0 -> 384-391 / 380-384 / 379-383 / 382-390 ms,
     // profiles/r03_tail_enter4.json)
-    double tail_enter = nl == 4 ? 1.4 : 2.0;
-    if (const char* e = getenv("RT_TAIL_ENTER")) tail_enter = atof(e);  // (sweeps)
+    const double tail_enter = sc.tail_enter >= 0.0 ? sc.tail_enter : nl == 4 ? 1.4 : 2.0;
     const long tail_max = (long)(tail_enter * tail_blocks * 4 * tail_p / nl);
     if (nl > 1) {
         HIPCHK(c, hipEventRecord(b->ev_fork, s));
@@ -1824,12 +1832,19 @@ int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounces, cons
         W.any_rays = b->any_rays;
         W.fb = lfb;
         W.fb_rs = fb_rs;
-        W.budget = b->budget;
+        W.budget = sc.step_budget > 0 ? sc.step_budget : b->budget;
         W.counters = La.cnt;
         W.tail_paths = tail_p;
         W.drain_rows = drain_rows;
         W.force_fb = force_fb;
         W.iterq = (S && iter_log && l == 0) ? (int32_t*)b->iterq.p : nullptr;
+        if (wlog) {
+            W.wlog_n = (int32_t*)b->wlog.p;
+            W.wlog = (float4_*)((char*)b->wlog.p + 256);
+            W.wlog_min = dg.wlog_min;
+            W.wlog_cap = dg.wlog_cap;
+            W.wlog_every = dg.wlog_every;
+        }
         La.lists[0] = (int32_t*)W.act_in;
         La.lists[1] = W.act_out;
         HIPCHK(c, hipMemsetAsync(La.cnt, 0, C_COUNT * sizeof(int32_t), La.s));
@@ -1839,9 +1854,9 @@ int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounces, cons
         hipLaunchKernelGGL(k_init, dim3((La.n + threads - 1) / threads), dim3(threads), 0, La.s, W);
         HIPCHK(c, hipGetLastError());
     }
-    if (getenv("RT_VERBOSE"))
+    if (dg.verbose)
         fprintf(stderr, "[rt] run_wave n=%d lanes=%d cus=%d trace_blocks=%d budget=%d\n", n, nl, dev_cus, trace_blocks,
-                b->budget);
+                L[0].W.budget);
 
     // A sample takes at most bounces + 1 iterations without fallbacks; an
     // exact walk delays its path by at least one iteration. The bound only
@@ -1871,23 +1886,19 @@ int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounces, cons
             for (int k = 0; k < 3; k++)
                 if (!La.tev[k][La.it]) HIPCHK(c, hipEventCreate(&La.tev[k][La.it]));
         if (T) HIPCHK(c, hipEventRecord(La.tev[0][La.it], La.s));
-        // sparse launches (few live paths: the launch ends with its longest walk) walk with rows
-        const bool rows = La.live < row_below;
         const dim3 g(trace_blocks_of(La));
         if (SEQ)
-            hipLaunchKernelGGL((rows ? k_trace<true, false, 16> : k_trace<true, false, 4>), g, dim3(threads), 0, La.s, W, par, stats);
+            hipLaunchKernelGGL((k_trace<true, false>), g, dim3(threads), 0, La.s, W, par, stats);
         else if (S)
-            hipLaunchKernelGGL((rows ? k_trace<true, true, 16> : k_trace<true, true, 4>), g, dim3(threads), 0, La.s, W, par, stats);
+            hipLaunchKernelGGL((k_trace<true, true>), g, dim3(threads), 0, La.s, W, par, stats);
         else
-            hipLaunchKernelGGL((rows ? k_trace<false, true, 16> : k_trace<false, true, 4>), g, dim3(threads), 0, La.s, W, par, stats);
+            hipLaunchKernelGGL((k_trace<false, true>), g, dim3(threads), 0, La.s, W, par, stats);
         if (T) HIPCHK(c, hipEventRecord(La.tev[1][La.it], La.s));
         HIPCHK(c, hipGetLastError());
         return RT_OK;
     };
     auto launch_step = [&](WaveLane& La) -> int {
         const int par = La.it & 1;
-        La.W.spec_cam = (spec_cam && spec_dense > 0 && La.live > spec_dense) ? 2
-                        : (La.live < spec_sparse) ? 0 : spec_cam;
         if (S)
             hipLaunchKernelGGL(k_step<true>, dim3(step_blocks_of(La)), dim3(threads), 0, La.s, La.W, par, stats);
         else
@@ -1967,7 +1978,7 @@ int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounces, cons
             WaveLane& La = L[l];
             if (La.await) {
                 any = true;
-                const hipError_t q = host_blocking ? hipEventSynchronize(La.ev) : hipEventQuery(La.ev);
+                const hipError_t q = hipEventQuery(La.ev);
                 if (q == hipErrorNotReady) continue;
                 HIPCHK(c, q);
                 if (int r = process(La)) return r;
@@ -2002,6 +2013,16 @@ int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounces, cons
     b->tail_iter = L[0].tail_iter;
     HIPCHK(c, hipEventRecord(b->ev_done, s));
     b->done_recorded = true;
+    if (wlog) {  // (diagnostics: device 0's records of this render replace the last render's)
+        int32_t nw = 0;
+        HIPCHK(c, hipMemcpyAsync(&nw, b->wlog.p, 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(c, hipStreamSynchronize(s));
+        RtDiag& d = c->diag;
+        d.wlog_total = nw;
+        d.wlog.assign((size_t)std::min(nw, d.wlog_cap) * RT_WLOG_FLOATS, 0.0f);
+        if (!d.wlog.empty())
+            HIPCHK(c, hipMemcpy(d.wlog.data(), (char*)b->wlog.p + 256, d.wlog.size() * 4, hipMemcpyDeviceToHost));
+    }
     if (S && iter_log) {
         std::vector<int32_t> hq((size_t)6 * RT_MAX_TIMED_ITERS);
         HIPCHK(c, hipMemcpyAsync(hq.data(), b->iterq.p, hq.size() * 4, hipMemcpyDeviceToHost, s));
@@ -2037,7 +2058,8 @@ int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounces, cons
         // k_trace): lane, iteration, k_trace start, k_trace end = k_step start, k_step end,
         // 1 for the tail kernel (tools/timeline.py)
         // (device index d > 0 of a multi-device context writes file.d: the device threads run concurrently)
-        if (const char* tl = getenv("RT_TIMELINE")) {
+        if (!dg.timeline.empty()) {
+            const char* tl = dg.timeline.c_str();
             std::string rows;
             char line[128];
             for (int l = 0; l < nl; l++)

@@ -28,6 +28,12 @@
 
 namespace rtk {
 
+// Oriented slabs (rt_fast.h slab_ok) in the row walks: each lane also loads its record's
+// 16-B slab in the same round trip.
+#ifndef RT_SLAB_ROW
+#define RT_SLAB_ROW RT_SLABS
+#endif
+
 #define RT_DPP_ROW_MIRROR 0x140       // lane i <- lane 15 - i of its row
 #define RT_DPP_ROW_HALF_MIRROR 0x141  // lane i <- lane 7 - i of its half row
 #define RT_DPP_ROW_ROR(k) (0x120 + (k))  // lane i <- lane (i - k) mod 16 of its row
@@ -96,13 +102,21 @@ __device__ __forceinline__ int row_visit(const RtSceneView& S, QState& q, RSTK& 
     for (int dd = 0; dd < DESC && q.cur >= 0; dd++) {
         const float4_* p = (const float4_*)(S.bvh16 + (size_t)q.cur * RT_BVH16_W + sub);
         const float4_ a = p[0], b = p[1];
+#if RT_SLAB_ROW
+        const float4_ sl = S.bvh16s[(size_t)q.cur * RT_BVH16_W + sub];
+        rt_pin(sl);
+#endif
         rt_pin(a);
         rt_pin(b);
         const int ref = (int)rt_asuint(b.z), cnt = (int)rt_asuint(b.w);
         const float mn[3] = {a.x, a.y, a.z}, mx[3] = {a.w, b.x, b.y};
         const float tmax = ANY ? __builtin_inff() : h.t + h.t * RT_T2_WINDOW;
-        float tn;
-        const bool ok = cnt >= 0 && box_hit(mn, mx, q.rb, tmax, tn) && (ANY || tn <= tmax);
+        float tn, tf;
+#if RT_SLAB_ROW
+        const bool ok = cnt >= 0 && box_hit2(mn, mx, q.rb, tmax, tn, tf) && (ANY || tn <= tmax) && slab_ok(sl, q.o, q.d, tn, tf);
+#else
+        const bool ok = cnt >= 0 && box_hit2(mn, mx, q.rb, tmax, tn, tf) && (ANY || tn <= tmax);
+#endif
         const int item = cnt > 0 ? leaf_item(ref, cnt) : ref;
         const unsigned m = row_bits(__ballot(ok));
         const int nv = __popc(m);

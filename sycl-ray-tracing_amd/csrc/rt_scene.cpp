@@ -17,6 +17,8 @@
 
 namespace rt {
 
+std::atomic<long> g_obj_parallel_min{-1};
+
 int worker_count()
 {
     for (const char* v : {"RT_HOST_THREADS", "OMP_NUM_THREADS"})
@@ -314,8 +316,8 @@ int load_obj(const std::string& path, Mesh& out, std::string& err)
         return -1;
     }
     const int workers = worker_count();
-    size_t par_min = 4u << 20;  // (RT_OBJ_PARALLEL_MIN: tests force the chunked path on small files)
-    if (const char* e = std::getenv("RT_OBJ_PARALLEL_MIN")) par_min = (size_t)std::atol(e);
+    const long pm = g_obj_parallel_min.load();  // (rt_test_obj_parallel_min: tests force the chunked path)
+    const size_t par_min = pm >= 0 ? (size_t)pm : (size_t)4 << 20;
     if (text.size() < par_min || workers < 2) return load_obj_serial(path, out, err);
     out = Mesh();
     const char* T = text.data();
@@ -698,7 +700,7 @@ void build_octree(const float* tris, int ntris, int max_depth, int leaf_max, Oct
     }
     auto T0 = std::chrono::steady_clock::now();
     auto lap = [&](const char* what) {
-        if (!std::getenv("RT_BUILD_TIMES")) return;
+        if (!std::getenv("RT_VERBOSE")) return;
         auto T1 = std::chrono::steady_clock::now();
         std::fprintf(stderr, "[octree] %s %.1f ms\n", what, std::chrono::duration<double, std::milli>(T1 - T0).count());
         T0 = T1;
@@ -1157,7 +1159,7 @@ struct SahBuilder {
             process(nodes, t, st);
         }
         auto T0 = std::chrono::steady_clock::now();
-        if (std::getenv("RT_BUILD_TIMES"))
+        if (std::getenv("RT_VERBOSE"))
             std::fprintf(stderr, "[sah] top %.1f ms: %zu nodes, %zu deferred (cutoff %d)\n",
                          std::chrono::duration<double, std::milli>(T0 - T00).count(), nodes.size(), deferred.size(), cutoff);
         if (deferred.empty()) return;
@@ -1178,7 +1180,7 @@ struct SahBuilder {
                 process(nd, t, ls);
             }
         });
-        if (std::getenv("RT_BUILD_TIMES"))
+        if (std::getenv("RT_VERBOSE"))
             std::fprintf(stderr, "[sah] subtrees %.1f ms\n",
                          std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - T0).count());
         for (size_t k = 0; k < deferred.size(); k++) {
@@ -1337,11 +1339,154 @@ static void build_bvh16(const std::vector<Bvh4Node>& b4, std::vector<Bvh4Child>&
     });
 }
 
+// f32 <-> f16 bits (round to nearest even; finite inputs of magnitude <= 1 here)
+static uint16_t f16_bits(float f)
+{
+    uint32_t x;
+    std::memcpy(&x, &f, 4);
+    const uint32_t sign = (x >> 16) & 0x8000u;
+    const int exp = (int)((x >> 23) & 0xff) - 127 + 15;
+    uint32_t man = x & 0x7fffffu;
+    if (exp <= 0) {  // subnormal half (or zero)
+        if (exp < -10) return (uint16_t)sign;
+        man |= 0x800000u;
+        const int shift = 14 - exp;
+        uint32_t h = man >> shift;
+        const uint32_t rem = man & ((1u << shift) - 1u), half = 1u << (shift - 1);
+        if (rem > half || (rem == half && (h & 1u))) h++;
+        return (uint16_t)(sign | h);
+    }
+    uint32_t h = ((uint32_t)exp << 10) | (man >> 13);
+    const uint32_t rem = man & 0x1fffu;
+    if (rem > 0x1000u || (rem == 0x1000u && (h & 1u))) h++;
+    return (uint16_t)(sign | h);
+}
+
+// Oriented slabs of the search BVH's children (rt_fast.h slab_ok): a child's subtree covers a
+// contiguous run of bvh_tri4 (the SAH build partitions the triangles in place), whose
+// area-weighted mean normal n (when the normals do not cancel: |sum| > half the summed
+// areas) quantized to f16 gives the slab {x : lo <= n.x <= hi} over the run's vertices
+// a, a + e1, a + e2 (exactly the triangle Moller-Trumbore tests), widened by a margin that
+// covers the kernel's f32 evaluation of n.o + t n.d along any ray inside the scene's box and
+// the Moller-Trumbore hit's distance from its triangle's plane (~2e-6 of the
+// scene's magnitude; the margin is 1e-4 of the child's magnitude + 1e-5 of the scene's).
+// A ray segment inside the child's box that lies entirely on one side of the slab cannot
+// reach a hit there: such children are not entered. Grazing rays above a curved tessellated
+// surface enter many boxes but few slabs (the long search-BVH walks, profiles/r05_walk_*).
+void build_slabs(FlatBvh& out)
+{
+    const int nn = (int)out.bvh4.size();
+    const int nt = (int)(out.bvh_tri4.size() / 3);
+    out.bvh4s.assign((size_t)nn * 4, float4_{0.0f, 0.0f, -INFINITY, INFINITY});
+    out.bvh16s.assign((size_t)nn * RT_BVH16_W, float4_{0.0f, 0.0f, -INFINITY, INFINITY});
+    if (nn == 0 || nt == 0) return;
+    // triangle runs of every node (children's runs are adjacent)
+    std::vector<int> lo(nn, INT32_MAX), hi(nn, 0);
+    std::vector<int> order;  // post-order
+    {
+        std::vector<std::pair<int, int>> st{{0, 0}};
+        while (!st.empty()) {
+            auto& [v, k] = st.back();
+            if (k < 4) {
+                const Bvh4Child& c = out.bvh4[v].ch[k++];
+                if (c.cnt == 0) st.push_back({c.ref, 0});
+                continue;
+            }
+            order.push_back(v);
+            st.pop_back();
+        }
+    }
+    for (int v : order)
+        for (const Bvh4Child& c : out.bvh4[v].ch) {
+            if (c.cnt < 0) continue;
+            const int f = c.cnt > 0 ? c.ref : lo[c.ref], l = c.cnt > 0 ? c.ref + c.cnt : hi[c.ref];
+            lo[v] = std::min(lo[v], f), hi[v] = std::max(hi[v], l);
+        }
+    // prefix sums of the (double) normals cross(e1, e2) and their lengths
+    std::vector<double> ps((size_t)(nt + 1) * 4, 0.0);
+    for (int k = 0; k < nt; k++) {
+        const float4_* r = &out.bvh_tri4[3 * (size_t)k];
+        const double e1[3] = {r[1].x, r[1].y, r[1].z}, e2[3] = {r[2].x, r[2].y, r[2].z};
+        const double cr[3] = {e1[1] * e2[2] - e1[2] * e2[1], e1[2] * e2[0] - e1[0] * e2[2], e1[0] * e2[1] - e1[1] * e2[0]};
+        for (int a = 0; a < 3; a++) ps[4 * (size_t)(k + 1) + a] = ps[4 * (size_t)k + a] + cr[a];
+        ps[4 * (size_t)(k + 1) + 3] = ps[4 * (size_t)k + 3] + std::sqrt(cr[0] * cr[0] + cr[1] * cr[1] + cr[2] * cr[2]);
+    }
+    float scene_mag = 1.0f;
+    for (const Bvh4Child& c : out.bvh4[0].ch)
+        if (c.cnt >= 0)
+            for (int a = 0; a < 3; a++) scene_mag = std::max(scene_mag, std::max(std::fabs(c.lo[a]), std::fabs(c.hi[a])));
+    auto slab_of = [&](const Bvh4Child& c) -> float4_ {
+        float4_ s{0.0f, 0.0f, -INFINITY, INFINITY};
+        if (c.cnt < 0) return s;
+        const int f = c.cnt > 0 ? c.ref : lo[c.ref], l = c.cnt > 0 ? c.ref + c.cnt : hi[c.ref];
+        double m[3];
+        for (int a = 0; a < 3; a++) m[a] = ps[4 * (size_t)l + a] - ps[4 * (size_t)f + a];
+        const double area = ps[4 * (size_t)l + 3] - ps[4 * (size_t)f + 3];
+        const double len = std::sqrt(m[0] * m[0] + m[1] * m[1] + m[2] * m[2]);
+        if (!(len > 0.5 * area) || !(len > 0.0)) return s;
+        uint16_t hb[3];
+        double n[3];
+        for (int a = 0; a < 3; a++) {
+            hb[a] = f16_bits((float)(m[a] / len));
+            // the quantized component as the kernel decodes it
+            const uint32_t e = (hb[a] >> 10) & 31u, man = hb[a] & 1023u;
+            const double mag = e == 0 ? std::ldexp((double)man, -24) : std::ldexp((double)(1024u + man), (int)e - 25);
+            n[a] = (hb[a] & 0x8000u) ? -mag : mag;
+        }
+        double dlo = INFINITY, dhi = -INFINITY;
+        for (int k = f; k < l; k++) {
+            const float4_* r = &out.bvh_tri4[3 * (size_t)k];
+            const double av[3] = {r[0].x, r[0].y, r[0].z};
+            const double e1[3] = {r[1].x, r[1].y, r[1].z}, e2[3] = {r[2].x, r[2].y, r[2].z};
+            const double p0 = n[0] * av[0] + n[1] * av[1] + n[2] * av[2];
+            const double p1 = p0 + n[0] * e1[0] + n[1] * e1[1] + n[2] * e1[2];
+            const double p2 = p0 + n[0] * e2[0] + n[1] * e2[1] + n[2] * e2[2];
+            dlo = std::min(dlo, std::min(p0, std::min(p1, p2)));
+            dhi = std::max(dhi, std::max(p0, std::max(p1, p2)));
+        }
+        float cmag = 1.0f;
+        for (int a = 0; a < 3; a++) cmag = std::max(cmag, std::max(std::fabs(c.lo[a]), std::fabs(c.hi[a])));
+        const double margin = 1e-4 * cmag + 1e-5 * scene_mag;
+        const uint32_t w0 = (uint32_t)hb[0] | ((uint32_t)hb[1] << 16), w1 = hb[2];
+        std::memcpy(&s.x, &w0, 4);
+        std::memcpy(&s.y, &w1, 4);
+        s.z = (float)(dlo - margin);
+        s.w = (float)(dhi + margin);
+        // (float rounding of the bounds outwards)
+        if ((double)s.z > dlo - margin) s.z = std::nextafter(s.z, -INFINITY);
+        if ((double)s.w < dhi + margin) s.w = std::nextafter(s.w, INFINITY);
+        return s;
+    };
+    const int nw = worker_count();
+    parallel_for(std::min(nn, 4 * nw), nw, [&](int w) {
+        const int W = std::min(nn, 4 * nw);
+        for (int i = (int)((long)nn * w / W); i < (int)((long)nn * (w + 1) / W); i++)
+            for (int c = 0; c < 4; c++) out.bvh4s[4 * (size_t)i + c] = slab_of(out.bvh4[i].ch[c]);
+    });
+    // bvh16 order (build_bvh16): node i's leaf children, then its inner children's children
+    parallel_for(nw, nw, [&](int w) {
+        for (int i = (int)((long)nn * w / nw); i < (int)((long)nn * (w + 1) / nw); i++) {
+            float4_* rec = &out.bvh16s[(size_t)i * RT_BVH16_W];
+            int m = 0;
+            for (int c = 0; c < 4; c++) {
+                const Bvh4Child& ch = out.bvh4[i].ch[c];
+                if (ch.cnt < 0) continue;
+                if (ch.cnt > 0) {
+                    rec[m++] = out.bvh4s[4 * (size_t)i + c];
+                } else {
+                    for (int g = 0; g < 4; g++)
+                        if (out.bvh4[ch.ref].ch[g].cnt >= 0) rec[m++] = out.bvh4s[4 * (size_t)ch.ref + g];
+                }
+            }
+        }
+    });
+}
+
 void build_search_bvh(FlatBvh& out)
 {
     auto T0 = std::chrono::steady_clock::now();
     auto lap = [&](const char* what) {
-        if (!std::getenv("RT_BUILD_TIMES")) return;
+        if (!std::getenv("RT_VERBOSE")) return;
         auto T1 = std::chrono::steady_clock::now();
         std::fprintf(stderr, "[search bvh] %s %.1f ms\n", what, std::chrono::duration<double, std::milli>(T1 - T0).count());
         T0 = T1;
@@ -1401,6 +1546,8 @@ void build_search_bvh(FlatBvh& out)
     out.bvh4_ntop = bvh4_top_first(out.bvh4, 256);
     build_bvh16(out.bvh4, out.bvh16);
     lap("collapse");
+    build_slabs(out);
+    lap("slabs");
 }
 
 // ======================================================================= env

@@ -10,6 +10,8 @@
 // and adds the GPU flattening (layout described in DESIGN.md §3).
 #pragma once
 
+#include <atomic>
+
 #include <cstdint>
 #include <functional>
 #include <string>
@@ -54,6 +56,9 @@ void build_octree_serial(const float* tris, int ntris, int max_depth, int leaf_m
 // Host worker threads for scene preparation: OMP_NUM_THREADS / RT_HOST_THREADS if
 // set, else the hardware threads (at most 16: a GPU box's CPU share).
 int worker_count();
+// the OBJ size from which load_obj parses in chunks on worker threads (-1: the default,
+// 4 MB); tests set 0 through rt_test_obj_parallel_min to run the chunked path on small files
+extern std::atomic<long> g_obj_parallel_min;
 // fn(task) for task in [0, n) on up to `workers` threads (dynamic, one task at a time).
 void parallel_for(int n, int workers, const std::function<void(int)>& fn);
 // Pre-order dump identical to oracle/ref/ref_driver.cpp "bvh".
@@ -77,6 +82,8 @@ struct FlatBvh {
     int bvh4_ntop = 0;
     // 16-wide form (two bvh4 levels per node, rt_device.h Bvh16): 16 child records per node
     std::vector<Bvh4Child> bvh16;
+    // oriented slab per child record (build_slabs): {f16 normal x | y << 16, f16 normal z, lo, hi}
+    std::vector<float4_> bvh4s, bvh16s;
     std::vector<float4_> bvh_tri4;
 };
 void flatten_octree(const Octree& t, const float* tris, int ntris, FlatBvh& out);
@@ -84,6 +91,9 @@ void flatten_octree(const Octree& t, const float* tris, int ntris, FlatBvh& out)
 // any triangle the reference's Moller-Trumbore test reports as hit lies in
 // the boxes the traversal enters.
 void build_search_bvh(FlatBvh& out);
+// Oriented slabs of the search BVH's children (out.bvh4s / bvh16s), from bvh4, bvh16 and
+// bvh_tri4; build_search_bvh calls it.
+void build_slabs(FlatBvh& out);
 
 // ------------------------------------------------------------------ env
 // lum[i] = (float)(0.3086*r + 0.6094*g + 0.0820*b) in double (image.h:80-85)

@@ -121,6 +121,10 @@ struct WaveView {
     float* fspill_k;
     int fspill_lanes;
     int32_t* iterq;         // stats renders: [iteration][2] = {queries, live slots} (else null)
+    float4_* wlog;          // stats renders with a walk log (rt_test_walk_log): 3 float4 per long walk, else null
+    int32_t* wlog_n;        // records written (may exceed wlog_cap: the rest are dropped)
+    int wlog_min, wlog_cap; // quad_visit calls a logged walk takes at least; records at most
+    int wlog_every;         // 1, or a sampling modulus over (slot, iteration, kind)
     int iter;               // iteration of this launch
     int tail_paths;         // k_tail: paths per wave
     int drain_rows;         // k_trace: a wave's drain continues its walks as rows when at most this many remain
@@ -185,6 +189,12 @@ inline size_t wave_carve(char* base, size_t n, WaveView& W)  // uses W.park_cap,
     return o;
 }
 
+// The test stressor of rt_test_schedule("force_fallback", k): a query whose ray hashes to
+// 0 mod k skips the search-BVH walk for the exact octree walk (k = 0: off).
+RT_HD bool forced_fallback(int k, const float4_& o, const float4_& d)
+{
+    return k > 0 && ((rt_asuint(o.x) ^ rt_asuint(d.y) ^ (rt_asuint(d.z) >> 7)) % (uint32_t)k) == 0u;
+}
 RT_HD float4_ f4(V3 v, float w) { return float4_{v.x, v.y, v.z, w}; }
 RT_HD float4_ f4(Col c, float w) { return float4_{c.r, c.g, c.b, w}; }
 RT_HD V3 v3of(const float4_& f) { return v3(f.x, f.y, f.z); }

@@ -328,6 +328,39 @@ class RenderKernel:
         """Tests only (rt_test_fail_device): later multi-device renders fail `device` (-1: off)."""
         check(self.L, self.L.rt_test_fail_device(self.ctx, int(device)), self.ctx, "rt_test_fail_device")
 
+    def test_schedule(self, **params):
+        """Tests and measurement tools only (rt_test_schedule): override wavefront-schedule
+        parameters of the later renders, e.g. test_schedule(lanes=2, tail_paths=0,
+        force_fallback=7); reset=1 restores the product's schedule. No parameter changes
+        a result."""
+        for k, v in params.items():
+            check(self.L, self.L.rt_test_schedule(self.ctx, k.encode(), float(v)), self.ctx, "rt_test_schedule")
+
+    def test_walk_log(self, min_calls: int, capacity: int = 1 << 20, sample_every: int = 1):
+        """Tests and diagnostics only (rt_test_walk_log): stats renders record every walk of at
+        least min_calls quad_visit calls (0: off), or every sample_every-th by a hash."""
+        check(self.L, self.L.rt_test_walk_log(self.ctx, int(min_calls), int(sample_every), int(capacity)), self.ctx,
+              "rt_test_walk_log")
+        self._wlog_cap = int(capacity)
+
+    def walk_log(self) -> tuple[np.ndarray, int]:
+        """The last stats render's walk records as a structured array, and how many walks
+        qualified (include/rt_hip.h rt_test_walk_log)."""
+        cap = getattr(self, "_wlog_cap", 0)
+        raw = np.zeros((max(cap, 1), 12), np.float32)
+        total = int(self.L.rt_test_walk_log_read(self.ctx, ptr(raw), cap))
+        if total < 0:
+            check(self.L, total, self.ctx, "rt_test_walk_log_read")
+        raw = raw[:min(total, cap)]
+        iv = raw.view(np.int32)
+        dt = np.dtype([("o", np.float32, 3), ("kind", np.int32), ("where", np.int32), ("d", np.float32, 3),
+                       ("calls", np.int32), ("t", np.float32), ("tri", np.int32), ("iter", np.int32), ("slot", np.int32)])
+        out = np.zeros(raw.shape[0], dt)
+        out["o"], out["kind"], out["where"] = raw[:, 0:3], iv[:, 3] & 0xff, iv[:, 3] >> 8
+        out["d"], out["calls"], out["t"] = raw[:, 4:7], iv[:, 7], raw[:, 8]
+        out["tri"], out["iter"], out["slot"] = iv[:, 9], iv[:, 10], iv[:, 11]
+        return out, total
+
     def set_stats(self, on):
         """True / 1: counters of the next renders; 2: the same with unpaired occlusion walks
         (the box tests a walk must make: same answers); False / 0: off."""

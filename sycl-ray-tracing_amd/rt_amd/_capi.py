@@ -24,7 +24,8 @@ EXPORTS = [
     "rt_mesh_load", "rt_mesh_counts", "rt_mesh_copy", "rt_mesh_free", "rt_camera_preset", "rt_env_luminance_cdf",
     "rt_octree_dump", "rt_read_hdr", "rt_write_png", "rt_image_to_rgba8",
     "rt_set_intersect_mode", "rt_create_multi", "rt_device_count", "rt_set_materials", "rt_render_variants",
-    "rt_create_multi_loopback", "rt_test_fail_device",
+    "rt_create_multi_loopback", "rt_test_fail_device", "rt_test_schedule", "rt_test_walk_log",
+    "rt_test_walk_log_read", "rt_test_obj_parallel_min",
 ]
 
 # return codes (include/rt_hip.h)
@@ -40,6 +41,10 @@ _SIGS = {
     "rt_create_multi": (I, [I, P, ctypes.POINTER(P)]),
     "rt_create_multi_loopback": (I, [I, P, ctypes.POINTER(P)]),
     "rt_test_fail_device": (I, [P, I]),
+    "rt_test_schedule": (I, [P, ctypes.c_char_p, ctypes.c_double]),
+    "rt_test_walk_log": (I, [P, I, I, I]),
+    "rt_test_walk_log_read": (L, [P, P, L]),
+    "rt_test_obj_parallel_min": (I, [L]),
     "rt_device_count": (I, [P]),
     "rt_set_materials": (I, [P, P, I]),
     "rt_destroy": (None, [P]),

@@ -84,9 +84,12 @@ def make_kernel(entry: dict, cameras: dict, hostsim: bool, W=None, H=None, spp=N
     return rk, fb
 
 
-def run_case(entry: dict, cameras: dict, hostsim: bool) -> np.ndarray:
-    """Returns the tone-mapped RGBA of the case (full frame or its pixel list)."""
+def run_case(entry: dict, cameras: dict, hostsim: bool, schedule: dict | None = None) -> np.ndarray:
+    """Returns the tone-mapped RGBA of the case (full frame or its pixel list); schedule:
+    rt_test_schedule overrides (tests only)."""
     rk, fb = make_kernel(entry, cameras, hostsim)
+    if schedule:
+        rk.test_schedule(**schedule)
     if entry.get("px") is None:
         rk.render()
         return fb.pixels

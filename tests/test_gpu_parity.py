@@ -263,7 +263,7 @@ def test_gpu_slab_division_exact():
     assert same.all(), (a[~same][:4], d[~same][:4])
 
 
-def test_gpu_schedules_bit_identical(monkeypatch):
+def test_gpu_schedules_bit_identical():
     """The frame does not depend on the schedule: 1-4 wavefront lanes, the
     tail kernel on or off (1-8 paths per wave, entered at once or late), quad or
     row walks (rt_row.h) in the tail kernel and in k_trace, row
@@ -276,22 +276,12 @@ def test_gpu_schedules_bit_identical(monkeypatch):
     sky = scenes.make_sky("L")
     W, H, spp, nb = 640, 480, 2, 8
 
-    def render(lanes, tail, off=0, stride=1, heavy=6, enter=2.0, spec_cam=1, rows=1, row_below=0, drain=4,
-               tail_cam=0, dense=0, sparse=0):
-        monkeypatch.setenv("RT_TAIL_SPEC_CAM", str(tail_cam))
-        monkeypatch.setenv("RT_SPEC_CAM_DENSE", str(dense))
-        monkeypatch.setenv("RT_SPEC_CAM_SPARSE", str(sparse))
-        monkeypatch.setenv("RT_DRAIN_ROWS", str(drain))
-        monkeypatch.setenv("RT_TAIL_ROWS", str(rows))
-        monkeypatch.setenv("RT_ROW_BELOW", str(row_below))
-        monkeypatch.setenv("RT_LANES", str(lanes))
-        monkeypatch.setenv("RT_TAIL_PATHS", str(tail))
-        monkeypatch.setenv("RT_HEAVY", str(heavy))
-        monkeypatch.setenv("RT_TAIL_ENTER", str(enter))
-        monkeypatch.setenv("RT_SPEC_CAM", str(spec_cam))
+    def render(lanes, tail, off=0, stride=1, heavy=6, enter=2.0, spec_cam=1, rows=1, drain=4, tail_cam=0):
         rk = rt_amd.RenderKernel(W, H, spp, nb, rt_amd.Image(1, 1), P.triangles, P.materials,
                                  P.emissive_triangle_indices, P.material_indices, None, rt_amd.BVH(P.triangles),
                                  rt_amd.Image.from_rgb(sky), None, device=0)
+        rk.test_schedule(lanes=lanes, tail_paths=tail, heavy_calls=heavy, tail_enter=enter, spec_cam=spec_cam,
+                         tail_rows=rows, drain_rows=drain, tail_spec_cam=tail_cam)
         rk.set_camera(rt_amd.Camera.preset("dragon"))
         rows = len(range(off, H, stride))
         init = np.zeros((rows, W, 4), np.float32)
@@ -318,23 +308,20 @@ def test_gpu_schedules_bit_identical(monkeypatch):
         got = render(lanes, tail, enter=enter)
         np.testing.assert_array_equal(got.view(np.uint32), base.view(np.uint32),
                                       err_msg=f"lanes={lanes} tail={tail} enter={enter}")
-    # camera rays traced ahead: never, only where the pixel's previous sample ended (2), mode 2
-    # in launches above a live count, and the tail kernel's own mode
-    for lanes, tail, spec_cam, tail_cam, dense, sparse in ((1, 0, 0, 0, 0, 0), (3, 2, 0, 0, 0, 0), (1, 0, 2, 0, 0, 0),
-                                                           (3, 1, 2, 2, 0, 0), (3, 1, 1, 1, 0, 0), (3, 1, 1, 2, 0, 0),
-                                                           (2, 1, 1, 0, 50000, 0), (2, 0, 1, 0, 0, 60000),
-                                                           (3, 1, 1, 1, 120000, 30000)):
-        got = render(lanes, tail, spec_cam=spec_cam, tail_cam=tail_cam, dense=dense, sparse=sparse)
+    # camera rays traced ahead: never, only where the pixel's previous sample ended (2), and the
+    # tail kernel's own mode
+    for lanes, tail, spec_cam, tail_cam in ((1, 0, 0, 0), (3, 2, 0, 0), (1, 0, 2, 0), (3, 1, 2, 2), (3, 1, 1, 1),
+                                            (3, 1, 1, 2)):
+        got = render(lanes, tail, spec_cam=spec_cam, tail_cam=tail_cam)
         np.testing.assert_array_equal(got.view(np.uint32), base.view(np.uint32),
-                                      err_msg=f"spec_cam={spec_cam} tail_cam={tail_cam} dense={dense} "
-                                              f"sparse={sparse} lanes={lanes}")
-    # the walks by quads or by rows (rt_row.h) in the tail kernel, and rows in every k_trace launch
-    # (and a k_trace drain continuing its quad walks as rows, or not; 1 walk at most, or 4)
-    for rows, row_below, tail, enter, drain in ((0, 0, 2, 2.0, 0), (1, 0, 1, 1000.0, 1), (1, 1 << 30, 1, 2.0, 4),
-                                                (0, 1 << 30, 4, 2.0, 0), (1, 0, 0, 2.0, 4), (1, 0, 0, 2.0, 1)):
-        got = render(3, tail, enter=enter, rows=rows, row_below=row_below, drain=drain)
+                                      err_msg=f"spec_cam={spec_cam} tail_cam={tail_cam} lanes={lanes}")
+    # the walks by quads or by rows (rt_row.h) in the tail kernel (and a k_trace drain continuing
+    # its quad walks as rows, or not; 1 walk at most, or 4)
+    for rows, tail, enter, drain in ((0, 2, 2.0, 0), (1, 1, 1000.0, 1), (1, 1, 2.0, 4), (0, 4, 2.0, 0), (1, 0, 2.0, 4),
+                                     (1, 0, 2.0, 1)):
+        got = render(3, tail, enter=enter, rows=rows, drain=drain)
         np.testing.assert_array_equal(got.view(np.uint32), base.view(np.uint32),
-                                      err_msg=f"rows={rows} row_below={row_below} tail={tail}")
+                                      err_msg=f"rows={rows} tail={tail} drain={drain}")
 
 
 @pytest.mark.gpu
@@ -348,20 +335,18 @@ def test_gpu_tiny_scenes_match_oracle(n, cameras):
 
 @pytest.mark.parametrize("tail", ["0", "5"])
 @pytest.mark.parametrize("name,budget,every", [("mis_512", 1, 7), ("cornell32_128", 1, 7), ("cfg2_dragon", 8, 31)])
-def test_gpu_parked_walks_small_launches(name, budget, every, tail, manifest, cameras, monkeypatch):
+def test_gpu_parked_walks_small_launches(name, budget, every, tail, manifest, cameras):
     """Exact-walk hand-off under stress: every `every`-th query (by
-    a hash of its ray, RT_FORCE_FALLBACK) skips the quad walk for the exact
+    a hash of its ray, rt_test_schedule force_fallback) skips the quad walk for the exact
     octree walk, a step budget of 1 (8 on the dragon, whose walks take ~200
     steps: each park costs an iteration) parks those walks at node
     boundaries, and with the tail kernel off the last iterations run k_step on
     a live count of a few paths while fallbacks and parked walks are pending
     (with it on, k_tail walks them inline). Every pixel must still be written,
     bit for bit the reference's."""
-    monkeypatch.setenv("RT_STEP_BUDGET", str(budget))
-    monkeypatch.setenv("RT_TAIL_PATHS", tail)
-    monkeypatch.setenv("RT_FORCE_FALLBACK", str(every))
     e = rt_cases.golden_case(name, manifest)
     rk, fb = rt_cases.make_kernel(e, cameras, hostsim=False)
+    rk.test_schedule(step_budget=budget, tail_paths=int(tail), force_fallback=every)
     rk.set_stats(True)
     if e.get("px") is None:
         rk.render()

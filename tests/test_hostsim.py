@@ -26,15 +26,42 @@ def test_hostsim_render_bit_exact(name, manifest, cameras):
 
 
 @pytest.mark.parametrize("spec_cam", [0, 2])
-def test_hostsim_camera_ahead_policies_bit_exact(spec_cam, manifest, cameras, monkeypatch):
+def test_hostsim_camera_ahead_policies_bit_exact(spec_cam, manifest, cameras):
     """The next sample's camera ray traced ahead never (0) or only where the pixel's
     previous sample ended (2, rt_wave.h next_camera): which rays are cast changes, the
     answers do not."""
-    monkeypatch.setenv("RT_SPEC_CAM", str(spec_cam))
     for name in rt_cases.CORNELL_CASES[:2]:
         e = rt_cases.golden_case(name, manifest)
-        got = rt_cases.run_case(e, cameras, hostsim=True)
+        got = rt_cases.run_case(e, cameras, hostsim=True, schedule={"spec_cam": spec_cam})
         assert gio.compare_rgb(got, e["expected"])["bitwise_fraction"] == 1.0, name
+
+
+def test_schedule_is_not_read_from_the_environment(manifest, cameras, monkeypatch):
+    """Product hygiene: the test stressor that sends every k-th query to the exact
+    walk is a test-only C entry (rt_test_schedule), not an environment variable, so a stray
+    RT_FORCE_FALLBACK (or any other old schedule knob) in a user's environment changes nothing:
+    the fallback count with it set equals the count without; through rt_test_schedule the count
+    rises and the frame stays bitwise."""
+    e = rt_cases.golden_case(rt_cases.CORNELL_CASES[0], manifest)
+
+    def fallbacks(schedule=None):
+        rk, fb = rt_cases.make_kernel(e, cameras, hostsim=True)
+        rk.set_stats(True)
+        if schedule:
+            rk.test_schedule(**schedule)
+        rk.render()
+        assert gio.compare_rgb(fb.pixels, e["expected"])["bitwise_fraction"] == 1.0
+        return rk.stats()["fallback"]
+
+    base = fallbacks()
+    for k, v in (("RT_FORCE_FALLBACK", "3"), ("RT_STEP_BUDGET", "1"), ("RT_SPEC_CAM", "0"), ("RT_TAIL_PATHS", "0"),
+                 ("RT_LANES", "2"), ("RT_HEAVY", "1"), ("RT_DRAIN_ROWS", "0")):
+        monkeypatch.setenv(k, v)
+    assert fallbacks() == base
+    assert fallbacks({"force_fallback": 3}) > base
+    rk, _ = rt_cases.make_kernel(e, cameras, hostsim=True)
+    with pytest.raises(rt_amd.RtError):
+        rk.test_schedule(no_such_knob=1)
 
 
 @pytest.mark.slow

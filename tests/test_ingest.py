@@ -17,9 +17,21 @@ from conftest import load_golden
 import rt_amd
 
 
+@pytest.fixture
+def chunked():
+    """rt_test_obj_parallel_min: chunked(True) sends every file through the chunked parse, even
+    small ones; chunked(False) restores the default size threshold (also at the test's end)."""
+    L_ = rt_amd.lib()
+
+    def set_(on: bool):
+        L_.rt_test_obj_parallel_min(0 if on else -1)
+    yield set_
+    set_(False)
+
+
 @pytest.mark.parametrize("scene", ["cornell12", "cornell", "mis"])
-def test_chunked_parse_matches_reference(scene, monkeypatch):
-    monkeypatch.setenv("RT_OBJ_PARALLEL_MIN", "0")  # the chunked path even on small files
+def test_chunked_parse_matches_reference(scene, chunked):
+    chunked(True)  # the chunked path even on small files
     P = rt_amd.parse_obj(scenes.scene_path(scene))
     g = load_golden(f"parse_{scene}.npz")
     np.testing.assert_array_equal(P.triangles.reshape(-1).view(np.uint32), g["tris"].reshape(-1).view(np.uint32))
@@ -51,7 +63,7 @@ def _grid(n):
 
 @pytest.mark.parametrize("case", ["index_then_vertex", "vertex_then_index", "polygon", "ok", "index_then_parse_same_chunk",
                                   "polygon_with_bad_index", "index_then_mtllib", "mtllib_then_index", "short_face"])
-def test_chunked_parse_first_error_in_file_order(case, tmp_path, monkeypatch):
+def test_chunked_parse_first_error_in_file_order(case, tmp_path, chunked):
     lines = _grid(400)
     if case == "index_then_vertex":
         lines[100] = "f 1 2 99999"
@@ -76,14 +88,14 @@ def test_chunked_parse_first_error_in_file_order(case, tmp_path, monkeypatch):
         lines[900] = "f 1 2"
     path = _obj(tmp_path, lines)
     serial = _err(path)
-    monkeypatch.setenv("RT_OBJ_PARALLEL_MIN", "0")
-    chunked = _err(path)
-    assert chunked == serial
+    chunked(True)
+    got = _err(path)
+    assert got == serial
     if case == "ok":
         assert serial is None
-        monkeypatch.delenv("RT_OBJ_PARALLEL_MIN")
+        chunked(False)
         a = rt_amd.parse_obj(path)
-        monkeypatch.setenv("RT_OBJ_PARALLEL_MIN", "0")
+        chunked(True)
         b = rt_amd.parse_obj(path)
         np.testing.assert_array_equal(a.triangles, b.triangles)
     else:

@@ -29,7 +29,6 @@ def main():
     os.makedirs(os.path.dirname(args.out) or ".", exist_ok=True)
     prefix = f"{args.out}_{args.config}_w{args.world}"
     os.environ["RT_ITER_LOG"] = prefix
-    os.environ["RT_LANES"] = str(args.lanes)
     import numpy as np
     import torch
     import bench
@@ -41,6 +40,7 @@ def main():
                              P.emissive_triangle_indices, P.material_indices, None, rt_amd.BVH(P.triangles),
                              rt_amd.Image.from_rgb(sky), None, device=0)
     rk.set_camera(rt_amd.Camera(cam17[:16], cam17[16]))
+    rk.set_lanes(args.lanes)
     dev = torch.device("cuda", 0)
     fr = ShardedFrame(rk, 0, args.world, device=dev)
     stream = torch.cuda.current_stream(dev).cuda_stream

@@ -1,11 +1,11 @@
-"""Frame time of a cfg4 N-way shard and of the full cfg2 frame under several run_wave env
-settings, in one process (run_wave reads its knobs at every render).
+"""Frame time of a cfg4 N-way shard and of the full cfg2 frame under several wavefront
+schedules (rt_test_schedule keys), in one process.
 
-  python tools/knob_probe.py --sets "RT_TAIL_PATHS=2,RT_TAIL_ENTER=2" "RT_TAIL_PATHS=8,RT_TAIL_ENTER=2" \
+  python tools/knob_probe.py --sets - "tail_paths=2,tail_enter=2" "lanes=3" \
       [--world 8 --rank 1] [--reps 3] [--rounds 2] [--out gpurun_out/knob_probe.json]
 
-Settings alternate round by round (A B C A B C ...), min over reps per round. LANES=k sets the
-context's wavefront lanes (rt_device_set_lanes; default 0 = auto).
+Settings alternate round by round (A B C A B C ...), min over reps per round; "-" is the
+product's schedule.
 """
 from __future__ import annotations
 
@@ -45,21 +45,13 @@ def main():
     rk.set_camera(rt_amd.Camera(cam17[:16], cam17[16]))
     dev = torch.device("cuda", 0)
     stream = torch.cuda.current_stream(dev).cuda_stream
-    base_env = dict(os.environ)
 
     def apply(s):
-        for k in list(os.environ):
-            if k.startswith("RT_") and k not in base_env:
-                del os.environ[k]
-        lanes = 0  # (auto)
+        # a set: "-" (the product's schedule) or "key=value,..." of rt_test_schedule keys
+        # (lanes, tail_paths, tail_enter, tail_rows, drain_rows, heavy_calls, spec_cam, ...)
+        rk.test_schedule(reset=1)
         if s != "-":
-            for kv in s.split(","):
-                k, v = kv.split("=", 1)
-                if k == "LANES":  # (wavefront lanes of the context: rt_device_set_lanes)
-                    lanes = int(v)
-                else:
-                    os.environ[k] = v
-        rk.set_lanes(lanes)
+            rk.test_schedule(**{kv.split("=", 1)[0]: float(kv.split("=", 1)[1]) for kv in s.split(",")})
 
     def timed(cfg):
         if cfg == "cfg4":
@@ -90,7 +82,7 @@ def main():
                 res[s]["cfg2_ms"].append(round(ms2, 2))
             print(json.dumps({"round": rnd, "set": s, **{k: v[-1] for k, v in res[s].items() if v}}), flush=True)
     apply("-")
-    out = {"what": f"cfg4 rank {args.rank} of {args.world} shard and full cfg2 frame per env setting, min of "
+    out = {"what": f"cfg4 rank {args.rank} of {args.world} shard and full cfg2 frame per schedule setting (rt_test_schedule), min of "
                    f"{args.reps} renders per round, settings alternating over {args.rounds} rounds (one MI355X)",
            "results": res}
     os.makedirs(os.path.dirname(args.out) or ".", exist_ok=True)

@@ -69,6 +69,8 @@ def main():
 
     scene, sky_kind, cam, W, H, spp, nb, desc = bench.CONFIGS[args.config]
     P, sky, cam17 = bench.build_inputs(args.config)
+    os.makedirs(os.path.dirname(args.out) or ".", exist_ok=True)
+    os.environ["RT_TIMELINE"] = args.out + ".txt"  # (read when the context is created; written by timed renders)
     rk = rt_amd.RenderKernel(W, H, spp, nb, rt_amd.Image(1, 1), P.triangles, P.materials,
                              P.emissive_triangle_indices, P.material_indices, None, rt_amd.BVH(P.triangles),
                              rt_amd.Image.from_rgb(sky), None, device=0)
@@ -82,15 +84,12 @@ def main():
     fr.render(stream)
     torch.cuda.synchronize(dev)
     plain_ms = (time.perf_counter() - t0) * 1e3
-    os.makedirs(os.path.dirname(args.out) or ".", exist_ok=True)
-    os.environ["RT_TIMELINE"] = args.out + ".txt"
     rk.kernel_timing(1)
     t0 = time.perf_counter()
     fr.render(stream)
     torch.cuda.synchronize(dev)
     timed_ms = (time.perf_counter() - t0) * 1e3
     rk.kernel_timing(0)
-    del os.environ["RT_TIMELINE"]
     rows = np.loadtxt(args.out + ".txt", ndmin=2)
     s = summarize(rows)
     s.update({"config": args.config, "world": args.world, "rank": args.rank, "render_ms": round(plain_ms, 2),
