@@ -20,6 +20,8 @@ HIPFLAGS := -std=c++17 -O3 -fPIC --offload-arch=$(ARCH) -ffp-contract=off -fno-f
             -fno-gpu-flush-denormals-to-zero -fhip-fp32-correctly-rounded-divide-sqrt -Wall -Wno-unused-function -Wno-unknown-pragmas
 
 HDRS := $(wildcard $(SRC)/*.h) include/rt_hip.h
+# the kernel sources' hash, compiled into each library (rt_build_id) so a run reports the build it loaded
+SRC_HASH := $(shell cat $(SRC)/* include/*.h 2>/dev/null | sha256sum | cut -c1-12)
 
 all: $(LIB)/librt_hip.so $(LIB)/librt_hostsim.so oracle/liboracle.so build/libm_check build/cdf_check stamp
 
@@ -29,11 +31,11 @@ $(OBJ)/%.host.o: $(SRC)/%.cpp $(HDRS)
 
 $(OBJ)/rt_hostsim.o: $(SRC)/rt_hostsim.cpp $(HDRS)
 	@mkdir -p $(OBJ)
-	$(CXX) $(CXXFLAGS) -fopenmp -c $< -o $@
+	$(CXX) $(CXXFLAGS) -fopenmp -DRT_BUILD_SRC='"$(SRC_HASH)"' -c $< -o $@
 
 $(OBJ)/rt_render.o: $(SRC)/rt_render.hip $(HDRS)
 	@mkdir -p $(OBJ)
-	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+	$(HIPCC) $(HIPFLAGS) -DRT_BUILD_SRC='"$(SRC_HASH)"' -c $< -o $@
 
 $(LIB)/librt_hip.so: $(OBJ)/rt_render.o $(OBJ)/rt_scene.host.o $(OBJ)/rt_imageio.host.o $(OBJ)/rt_capi_host.host.o
 	@mkdir -p $(LIB)
@@ -73,7 +75,7 @@ clean:
 # experiment builds: make variant V=name DEFS="-DRT_TAIL_OCC=2" -> lib/librt_hip_name.so (RT_HIP_LIB=...)
 variant: $(OBJ)/rt_scene.host.o $(OBJ)/rt_imageio.host.o $(OBJ)/rt_capi_host.host.o
 	@mkdir -p $(LIB)
-	$(HIPCC) $(HIPFLAGS) $(DEFS) -c $(SRC)/rt_render.hip -o $(OBJ)/rt_render_$(V).o
+	$(HIPCC) $(HIPFLAGS) $(DEFS) -DRT_BUILD_SRC='"$(SRC_HASH)"' -DRT_BUILD_DEFS='"$(DEFS)"' -c $(SRC)/rt_render.hip -o $(OBJ)/rt_render_$(V).o
 	$(HIPCC) -shared --offload-arch=$(ARCH) -fPIC $(OBJ)/rt_render_$(V).o $^ -o $(LIB)/librt_hip_$(V).so
 
 # C++ drop-in check (container only): include/render_kernel_hip.h against the

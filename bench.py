@@ -225,11 +225,22 @@ def load_traffic(key):
 
 
 def build_commit():
-    """The commit librt_hip.so was built from (BUILD_COMMIT, written by `make` with the library)."""
+    """The build of the library this process loaded (its rt_build_id: the kernel sources' hash and
+    any experiment flags, compiled in by `make`), prefixed with the commit BUILD_COMMIT names when
+    that stamp is of the same sources."""
     try:
-        return open(os.path.join(REPO, "BUILD_COMMIT")).read().strip() or None
-    except OSError:
+        from rt_amd import _capi
+        lib_id = _capi.lib().rt_build_id().decode()
+    except Exception:  # noqa: BLE001  (no library: no build to report)
         return None
+    try:
+        stamp = open(os.path.join(REPO, "BUILD_COMMIT")).read().split()
+    except OSError:
+        stamp = []
+    src = lambda b: b.split("src=")[-1].split()[0] if b and "src=" in b else None  # noqa: E731
+    if len(stamp) >= 2 and src(stamp[1]) == src(lib_id):
+        return f"{stamp[0]} {lib_id}"
+    return lib_id
 
 
 def traffic_source(key):
@@ -242,7 +253,7 @@ def traffic_source(key):
     if e is None:
         return None
     now = build_commit()
-    src = lambda b: b.split("src=")[-1] if b and "src=" in b else None  # noqa: E731  (the kernel sources' hash)
+    src = lambda b: b.split("src=")[-1].split()[0] if b and "src=" in b else None  # noqa: E731  (the kernel sources' hash)
     return {"profile": e.get("profile"), "build": e.get("build"), "running_build": now,
             "same_build": bool(src(now) and src(now) == src(e.get("build")))}
 

@@ -92,6 +92,9 @@ long rt_test_walk_log_read(const rt_context* ctx, float* out, long capacity);
 void rt_destroy(rt_context* ctx);
 const char* rt_last_error(const rt_context* ctx); /* ctx may be NULL: last global error */
 int rt_version(void);
+/* The build of this library: "src=<hash of its kernel sources> defs=<experiment
+ * flags>" (Makefile), so a measurement reports the binary it ran. */
+const char* rt_build_id(void);
 
 /* Scene buffers bound by the RenderKernel constructor (render_kernel.h:27-31). */
 int rt_set_scene(rt_context* ctx, const float* triangles, int n_triangles, const int* material_indices,
@@ -175,8 +178,9 @@ int rt_set_intersect_mode(rt_context* ctx, int use_bvh);
  * gfx950 tail kernel (k_tail) in those totals. */
 /* enabled = 2: counters of a render whose occlusion walks take one node per trip
  * (the gfx950 walks otherwise pair the stack top's node into the same trip, testing
- * boxes a one-node walk may never reach): the box tests a walk must make, for the
- * roofline's necessary-bytes figure. Same answers, same frame. */
+ * boxes a one-node walk may never reach) and whose walks are all quad walks (no
+ * 16-wide row trips in k_trace's drains or the tail kernel): the box tests a walk
+ * must make, for the roofline's necessary-bytes figure. Same answers, same frame. */
 int rt_set_stats(rt_context* ctx, int enabled);
 int rt_get_stats(const rt_context* ctx, unsigned long long* out, int n);
 /* Average duration (ms) of the last render kernel measured with HIP events. */

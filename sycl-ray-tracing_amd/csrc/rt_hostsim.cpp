@@ -415,3 +415,11 @@ extern "C" int rt_hostsim_heap_order(const float* keys, int m, int* order_emul, 
     }
     return 0;
 }
+
+#ifndef RT_BUILD_SRC
+#define RT_BUILD_SRC "unknown"
+#endif
+#ifndef RT_BUILD_DEFS
+#define RT_BUILD_DEFS ""
+#endif
+extern "C" const char* rt_build_id(void) { return "src=" RT_BUILD_SRC " defs=" RT_BUILD_DEFS " (hostsim)"; }

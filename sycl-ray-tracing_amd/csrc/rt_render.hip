@@ -27,6 +27,7 @@
 #include <algorithm>
 
 #include <dlfcn.h>
+#include <chrono>
 #include <mutex>
 #include <thread>
 
@@ -258,6 +259,13 @@ __device__ __forceinline__ void flush_stats(const rtk::Stats& st, unsigned long 
 }
 
 // ------------------------------------------------------------------ kernels
+// Queue record base of (kind, heavy class, shard): a normal shard holds seg_cap records, a
+// heavy shard RT_QSHARDS / RT_HSHARDS seg_caps (it takes the input shards sh with sh % RT_HSHARDS = its index).
+__host__ __device__ __forceinline__ size_t qbase(bool heavy, int shard, size_t seg_cap)
+{
+    return heavy ? ((size_t)RT_QSHARDS + (size_t)shard * (RT_QSHARDS / RT_HSHARDS)) * seg_cap : (size_t)shard * seg_cap;
+}
+
 // Appends what the wave's lanes emitted to the queues and the live list of
 // parity pout, in the shard of the 64-item input chunk `base` (whole wave).
 // Shards take contiguous runs of the n_in inputs' chunks, so a queue read in
@@ -271,7 +279,6 @@ __device__ __forceinline__ void append_emit(const rtk::WaveView& W, int pout, in
     const unsigned long long lt = (lane_id() == 0) ? 0ull : (~0ull >> (64 - lane_id()));
     if (W.r_heavy) {  // heavy class on: the rays of a path flagged heavy go to its kind's heavy shard
         const int hs = sh % RT_HSHARDS;
-        const size_t hseg = ((size_t)RT_QSHARDS + (size_t)hs * (RT_QSHARDS / RT_HSHARDS)) * W.seg_cap;
         unsigned long long b[2 * rtk::RK_COUNT + 1];
 #pragma unroll
         for (int k = 0; k < rtk::RK_COUNT; k++) {
@@ -292,12 +299,9 @@ __device__ __forceinline__ void append_emit(const rtk::WaveView& W, int pout, in
         }
 #pragma unroll
         for (int k = 0; k < rtk::RK_COUNT; k++) {
-            const int kk = e.heavy ? rtk::RK_COUNT + k : k;
-            const int i = __shfl(r[k], 0) + __popcll(b[k] & lt);
             const int ih = __shfl(r[rtk::RK_COUNT + k], 0) + __popcll(b[rtk::RK_COUNT + k] & lt);
-            if ((e.mask >> k) & 1u) {
-                W.q[k][kk == k ? seg + i : hseg + ih] = e.rec(k, p);
-            }
+            const int i = __shfl(r[k], 0) + __popcll(b[k] & lt);
+            if ((e.mask >> k) & 1u) W.q[k][e.heavy ? qbase(true, hs, W.seg_cap) + ih : qbase(false, sh, W.seg_cap) + i] = e.rec(k, p);
         }
         const int a = __shfl(r[2 * rtk::RK_COUNT], 0) + __popcll(b[2 * rtk::RK_COUNT] & lt);
         if (e.active) W.act_out[seg + a] = p;
@@ -320,7 +324,7 @@ __device__ __forceinline__ void append_emit(const rtk::WaveView& W, int pout, in
 #pragma unroll
     for (int k = 0; k < rtk::RK_COUNT; k++) {
         const int i = __shfl(r[k], 0) + __popcll(b[k] & lt);
-        if ((e.mask >> k) & 1u) W.q[k][seg + i] = e.rec(k, p);
+        if ((e.mask >> k) & 1u) W.q[k][qbase(false, sh, W.seg_cap) + i] = e.rec(k, p);
     }
     const int a = __shfl(r[rtk::RK_COUNT], 0) + __popcll(b[rtk::RK_COUNT] & lt);
     if (e.active) W.act_out[seg + a] = p;
@@ -380,9 +384,8 @@ __device__ __forceinline__ rtk::RayRec queue_item_at(const rtk::WaveView& W, con
     rtk::RayRec* qk = W.q[0];
 #pragma unroll
     for (int k2 = 1; k2 < rtk::RK_COUNT; k2++) qk = s.kind == k2 ? W.q[k2] : qk;
-    // (heavy shard h: after the kind's RT_QSHARDS segments, RT_QSHARDS / RT_HSHARDS of them each)
-    const int seg0 = s.heavy ? RT_QSHARDS + s.shard * (RT_QSHARDS / RT_HSHARDS) : s.shard;
-    return qk[(size_t)seg0 * W.seg_cap + (g - pre[j])];
+    // (heavy shard h: after the kind's RT_QSHARDS segments, RT_QSHARDS / RT_HSHARDS seg_caps each)
+    return qk[qbase(s.heavy, s.shard, W.seg_cap) + (g - pre[j])];
 }
 
 // Path init: every slot seeds its RNG and emits its first camera ray (into Q[0], ACT[0]).
@@ -1764,8 +1767,10 @@ int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounces, cons
     // the tail kernel (tail_rows: its rounds wait for their slowest walk). cfg4 8-way shard, one
     // MI355X (profiles/r04c_row_probe.json, r04d_tail_probe.json): quads 380-382 ms; tail rows
     // 367-370; rows for whole k_trace launches below 32 K / 131 K paths 415 / 420-428 ms (removed).
-    const int tail_rows = sc.tail_rows >= 0 ? (sc.tail_rows != 0) : RT_TAIL_ROWS;
-    const int drain_rows = sc.drain_rows >= 0 ? sc.drain_rows : RT_DRAIN_ROWS;  // k_trace: a drain's walks continue as rows
+    // (counter renders with unpaired occlusion walks, SEQ: every walk a quad walk, so that the box
+    // tests counted are the ones a one-node-per-trip walk makes; a row trip tests 16)
+    const int tail_rows = SEQ ? 0 : sc.tail_rows >= 0 ? (sc.tail_rows != 0) : RT_TAIL_ROWS;
+    const int drain_rows = SEQ ? 0 : sc.drain_rows >= 0 ? sc.drain_rows : RT_DRAIN_ROWS;  // k_trace: a drain's walks continue as rows
     // (rows: one path per wave, its ~4 queries on the wave's 4 rows: shard 367 ms vs 2 / 3 paths
     // 373-378 / 373-375 at the same entry live count)
     const int tail_p = sc.tail_paths >= 0 ? std::min(RT_TAIL_MAXP, sc.tail_paths) : tail_rows ? 1 : 2;
@@ -1943,7 +1948,7 @@ int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounces, cons
                 const dim3 g(tail_blocks);
                 La.W.spec_cam = spec_cam ? tail_spec_cam : 0;  // (the lane's last launch)
                 if (SEQ)
-                    hipLaunchKernelGGL((tail_rows ? k_tail<true, false, 16> : k_tail<true, false, 4>), g, dim3(threads), 0, La.s, La.W, par, stats);
+                    hipLaunchKernelGGL((k_tail<true, false, 4>), g, dim3(threads), 0, La.s, La.W, par, stats);
                 else if (S)
                     hipLaunchKernelGGL((tail_rows ? k_tail<true, true, 16> : k_tail<true, true, 4>), g, dim3(threads), 0, La.s, La.W, par, stats);
                 else
@@ -1972,6 +1977,9 @@ int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounces, cons
     // lane's event (blocking in lane order left lanes idle 17-34 ms of a 367-ms cfg4 8-way
     // shard: profiles/r04e_tl.json; 379.5-380.2 -> 370.5-373.2 ms, cfg2 148.5-149.7 -> 148.0,
     // profiles/r04i_drain_probe.json).
+    // (a thread that finds no lane done for a while sleeps between polls: in a multi-device
+    // render every device thread polls like this, and the caller's host work shares the cores)
+    auto idle_since = std::chrono::steady_clock::now();
     for (;;) {
         bool any = false, moved = false;
         for (int l = 0; l < nl; l++) {
@@ -1996,7 +2004,13 @@ int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounces, cons
             }
         }
         if (!any) break;
-        if (!moved) std::this_thread::yield();
+        if (moved) {
+            idle_since = std::chrono::steady_clock::now();
+        } else if (std::chrono::steady_clock::now() - idle_since > std::chrono::microseconds(200)) {
+            std::this_thread::sleep_for(std::chrono::microseconds(10));
+        } else {
+            std::this_thread::yield();
+        }
     }
     for (int l = 0; l < nl; l++) {  // each lane's pixels tone-mapped after its last step
         hipLaunchKernelGGL(k_tonemap, dim3((L[l].n + threads - 1) / threads), dim3(threads), 0, L[l].s, L[l].W);
@@ -2506,3 +2520,11 @@ extern "C" int rt_device_set_lanes(rt_context* c, int lanes)
     for (Backend* b : grp(c)->dev) b->lanes = std::min(RT_MAX_LANES, lanes);
     return RT_OK;
 }
+
+#ifndef RT_BUILD_SRC
+#define RT_BUILD_SRC "unknown"
+#endif
+#ifndef RT_BUILD_DEFS
+#define RT_BUILD_DEFS ""
+#endif
+extern "C" const char* rt_build_id(void) { return "src=" RT_BUILD_SRC " defs=" RT_BUILD_DEFS " (gfx950)"; }

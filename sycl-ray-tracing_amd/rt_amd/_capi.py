@@ -18,7 +18,7 @@ HOSTSIM = os.path.join(LIB_DIR, "librt_hostsim.so")
 
 # every symbol declared in include/rt_hip.h (tests check the export table)
 EXPORTS = [
-    "rt_create", "rt_destroy", "rt_last_error", "rt_version", "rt_set_scene", "rt_build_bvh",
+    "rt_create", "rt_destroy", "rt_last_error", "rt_version", "rt_build_id", "rt_set_scene", "rt_build_bvh",
     "rt_set_bvh_preorder", "rt_bvh_dump", "rt_bvh_info", "rt_set_env", "rt_set_camera", "rt_render",
     "rt_render_device", "rt_render_pixels", "rt_intersect", "rt_set_stats", "rt_get_stats", "rt_last_kernel_ms",
     "rt_mesh_load", "rt_mesh_counts", "rt_mesh_copy", "rt_mesh_free", "rt_camera_preset", "rt_env_luminance_cdf",
@@ -50,6 +50,7 @@ _SIGS = {
     "rt_destroy": (None, [P]),
     "rt_last_error": (ctypes.c_char_p, [P]),
     "rt_version": (I, []),
+    "rt_build_id": (ctypes.c_char_p, []),
     "rt_set_scene": (I, [P, P, I, P, I, P, I, P, I, P, I]),
     "rt_build_bvh": (I, [P, I, I]),
     "rt_set_bvh_preorder": (I, [P, P, L]),

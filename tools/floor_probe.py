@@ -36,6 +36,8 @@ def main():
     stream = torch.cuda.current_stream(dev).cuda_stream
     fr.render(stream)
     torch.cuda.synchronize(dev)
+    plain = rk.device_last_kernel_ms()  # (no per-launch events)
+    plain_iters = rk.last_iterations()
     rk.kernel_timing(1)
     fr.render(stream)
     torch.cuda.synchronize(dev)
@@ -43,6 +45,8 @@ def main():
     frame = rk.device_last_kernel_ms()
     out = {"pixels": W * H, "spp": args.spp, "frame_ms": round(frame, 3), "kernel_ms": {k: [round(v[0], 3), int(v[1])] for k, v in kt.items()}}
     n = max(1, kt["trace"][1])
+    out["plain_frame_ms"] = round(plain, 3)
+    out["plain_per_iteration_us"] = round(plain * 1e3 / max(1, plain_iters), 1)
     out["per_iteration_us"] = {"trace": round(kt["trace"][0] * 1e3 / n, 1), "step": round(kt["step"][0] * 1e3 / n, 1),
                                "frame": round(frame * 1e3 / n, 1)}
     print(json.dumps(out))

@@ -500,7 +500,7 @@ bool child_hit(const N4& n, int c, const float* o, const float* d, const float* 
 
 // ---------------------------------------------------------------- walk
 struct WalkOut {
-    int trips, inner, leaves, tris;
+    int trips, inner, leaves, tris, empty_inner, empty_leaves;
     float t;
 };
 WalkOut walk(const Tree& tr, const std::vector<Tri>& T, const float* o3, const float* d3, bool any)
@@ -510,7 +510,7 @@ WalkOut walk(const Tree& tr, const std::vector<Tri>& T, const float* o3, const f
     const RayB rb = rayb_setup(o, d);
     (void)rb;
     const float inv[3] = {1.0f / d3[0], 1.0f / d3[1], 1.0f / d3[2]};
-    WalkOut w{0, 0, 0, 0, INFINITY};
+    WalkOut w{0, 0, 0, 0, 0, 0, INFINITY};
     struct E {
         int item;
         float key;
@@ -534,6 +534,7 @@ WalkOut walk(const Tree& tr, const std::vector<Tri>& T, const float* o3, const f
                 if (child_hit(n, c, o3, d3, inv, tmax, tr.slabs, tn) && tn <= tmax)
                     h[nh++] = {n.cnt[c] > 0 ? ~((n.ref[c] << 3) | n.cnt[c]) : n.ref[c], any ? 0.0f : tn};
             }
+            if (!nh) w.empty_inner++;
             if (nh) {
                 std::stable_sort(h, h + nh, [](const E& a, const E& b) { return a.key < b.key; });
                 for (int j = nh - 1; j >= 1; j--)
@@ -544,6 +545,8 @@ WalkOut walk(const Tree& tr, const std::vector<Tri>& T, const float* o3, const f
         } else {
             w.leaves++;
             const int v = ~cur, first = v >> 3, cnt = v & 7;
+            const float tb = t;
+            bool any_hit = false;
             for (int j = 0; j < cnt; j++) {
                 const Tri& x = T[tr.refs[first + j]];
                 const V3 a = v3(x.a[0], x.a[1], x.a[2]);
@@ -551,8 +554,13 @@ WalkOut walk(const Tree& tr, const std::vector<Tri>& T, const float* o3, const f
                 const V3 e2 = v3(x.c[0] - x.a[0], x.c[1] - x.a[1], x.c[2] - x.a[2]);
                 float th;
                 w.tris++;
-                if (tri_test_v(a, e1, e2, o, d, th) && th < t) t = th;
+                if (tri_test_v(a, e1, e2, o, d, th)) {
+                    any_hit = true;
+                    if (th < t) t = th;
+                }
             }
+            (void)tb;
+            if (!any_hit) w.empty_leaves++;
             if (any && t < INFINITY) break;
         }
         if (pop) {
@@ -652,7 +660,7 @@ int main(int argc, char** argv)
         }
         tr.build_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
         std::vector<int> trips[2], all;
-        double sum = 0, sum_inner = 0, sum_leaves = 0, sum_tris = 0;
+        double sum = 0, sum_inner = 0, sum_leaves = 0, sum_tris = 0, sum_ei = 0, sum_el = 0;
         long miss_mismatch = 0;
         for (size_t i = 0; i < nr; i++) {
             const float* r = &rays[8 * i];
@@ -665,10 +673,13 @@ int main(int argc, char** argv)
             sum_inner += w.inner;
             sum_leaves += w.leaves;
             sum_tris += w.tris;
+            sum_ei += w.empty_inner;
+            sum_el += w.empty_leaves;
             (void)miss_mismatch;
         }
-        std::fprintf(stderr, "%-12s inner %.2f leaves %.2f tris %.2f\n", v.c_str(), sum_inner / std::max<size_t>(1, nr),
-                     sum_leaves / std::max<size_t>(1, nr), sum_tris / std::max<size_t>(1, nr));
+        std::fprintf(stderr, "%-12s inner %.2f (no child entered %.2f) leaves %.2f (no hit %.2f) tris %.2f\n", v.c_str(),
+                     sum_inner / std::max<size_t>(1, nr), sum_ei / std::max<size_t>(1, nr), sum_leaves / std::max<size_t>(1, nr),
+                     sum_el / std::max<size_t>(1, nr), sum_tris / std::max<size_t>(1, nr));
         std::fprintf(stderr, "%-12s nodes %zu refs %ld splits %ld build %.2fs  mean %.2f  p50 %.0f p90 %.0f p99 %.0f p99.9 %.0f max %.0f\n",
                      v.c_str(), tr.n.size(), nrefs, splits, tr.build_s, sum / std::max<size_t>(1, nr), qtile(all, 0.5),
                      qtile(all, 0.9), qtile(all, 0.99), qtile(all, 0.999), qtile(all, 1.0));

@@ -6,8 +6,8 @@ set -o pipefail
 T=${1:-r03}
 mkdir -p gpurun_out
 PMC_DETAIL=1 tools/profile_roofline.sh gpurun_out/${T}_roof --config cfg2 || exit 1
-python3 tools/update_traffic.py gpurun_out/${T}_roof --build "$(cat BUILD_COMMIT 2>/dev/null)" || exit 1
-cp profiles/traffic.json gpurun_out/traffic.json
+python3 tools/update_traffic.py gpurun_out/${T}_roof --build "$(cat BUILD_COMMIT 2>/dev/null)" --commit-dir profiles/${T}_roof || exit 1
+cp profiles/traffic.json gpurun_out/traffic.json  # (then copy gpurun_out/${T}_roof to profiles/${T}_roof, the path it records)
 timeout -k 10 300 python -u bench.py > gpurun_out/${T}_bench_cfg2.json 2> gpurun_out/${T}_bench_cfg2.err || exit 1
 cat gpurun_out/${T}_bench_cfg2.json
 timeout -k 10 300 python -u bench.py --config cfg3 > gpurun_out/${T}_bench_cfg3.json 2> gpurun_out/${T}_bench_cfg3.err || exit 1
