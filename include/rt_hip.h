@@ -79,7 +79,9 @@ int rt_test_schedule(rt_context* ctx, const char* key, double value);
 /* TEST ONLY. Walk log of stats renders (rt_set_stats): every search-BVH walk of
  * at least min_calls quad_visit calls (a row trip counts 2) is recorded, up to
  * capacity records (min_calls 0: off); sample_every > 1 keeps only the walks
- * whose (path slot, iteration, kind) hash is 0 modulo it. A record is RT_WLOG_FLOATS floats:
+ * whose (path slot, iteration, kind) hash is 0 modulo it, sample_every < 0 only
+ * the k_trace walks left to the exact octree walk (their triangle field then
+ * says why: 1 a tie, 2 the octree chain check, 3 the bounded stack). A record is RT_WLOG_FLOATS floats:
  * origin xyz, kind | where << 8 (int bits; where 0 k_trace quads, 1 a k_trace
  * drain's rows, 2 k_tail), direction xyz, calls (int bits), t (closest: the
  * answer, -1 none, -2 left to the exact walk; occlusion: 1 occluded / 0 not),

@@ -206,7 +206,7 @@ int rt_test_walk_log(rt_context* c, int min_calls, int sample_every, int capacit
 {
     if (!c || min_calls < 0 || capacity < 0) return rt_fail(c, RT_ERR_ARG, "rt_test_walk_log: bad arguments");
     c->diag.wlog_min = min_calls;
-    c->diag.wlog_every = std::max(1, sample_every);
+    c->diag.wlog_every = sample_every < 0 ? -1 : std::max(1, sample_every);
     c->diag.wlog_cap = min_calls > 0 ? capacity : 0;
     c->diag.wlog.clear();
     c->diag.wlog_total = 0;

@@ -219,17 +219,20 @@ RT_HD void sort4(float* k, int* v)
 #endif
 
 struct FastHit {
-    float t, t2;  // closest M-T hit (-1: none), smallest other hit seen (window-bounded)
-    int k;        // leaf-order triangle of t
+    float t, t2;  // closest M-T hit (-1: none), smallest other hit distance above t seen (window-bounded)
+    int k;        // leaf-order triangle of t (among triangles tied at t in one octree leaf: the first in its list)
     int leaf;     // its octree leaf record
-    bool tie;     // another triangle hit at exactly t
+    bool tie;     // another triangle hit at exactly t in another octree leaf (brute force: anywhere)
     bool ovf;     // the bounded stack overflowed: answer unknown
     int prim;     // brute-force mode: original index of t's triangle, the lowest among the ties
 };
 
-// One M-T hit (t, leaf-order k, octree leaf, original index prim) into h:
-// closest, tie flag, second-closest; in brute-force mode (USE_BVH 0) a tie
-// goes to the lowest original index, as the reference's strict `<` loop does.
+// One M-T hit (t, leaf-order k, octree leaf, original index prim) into h: closest, second
+// distance, ties. Triangles tied at t inside ONE octree leaf are settled here: the reference
+// visits that leaf once and takes the first of them in its list (strict `<`, bvh.h:150-161),
+// i.e. the lowest leaf-order k (flatten_octree writes each leaf's list in order); ties across
+// leaves depend on its heap order, so they flag `tie` (the exact walk answers). In brute-force
+// mode (USE_BVH 0) a tie goes to the lowest original index, as the reference's loop does.
 RT_HD void fast_take(FastHit& h, float t, int k, int leaf, int prim, bool brute)
 {
     if (t < h.t) {
@@ -240,12 +243,20 @@ RT_HD void fast_take(FastHit& h, float t, int k, int leaf, int prim, bool brute)
         h.prim = prim;
         h.tie = false;
     } else if (t == h.t) {
-        h.tie = true;
-        h.t2 = t;
-        if (brute && prim < h.prim) {
-            h.k = k;
-            h.leaf = leaf;
-            h.prim = prim;
+        if (brute) {
+            h.tie = true;
+            if (prim < h.prim) {
+                h.k = k;
+                h.leaf = leaf;
+                h.prim = prim;
+            }
+        } else if (leaf == h.leaf) {
+            if (k < h.k) {
+                h.k = k;
+                h.prim = prim;
+            }
+        } else {
+            h.tie = true;
         }
     } else if (t < h.t2) {
         h.t2 = t;

@@ -391,6 +391,35 @@ int rt_backend_intersect(rt_context* c, const float* rays, int n, void* out)
     return RT_OK;
 }
 
+// The search-BVH closest-hit query the render's k_trace stage runs (rt_fast.h
+// fast_query_closest, with its verification), for tests/test_hostsim.py: out_t = the
+// answer's t (-1 no hit) or -2 when the exact octree walk must answer; out_k its
+// triangle's original index (-1 none). rays[n][6] = origin, direction.
+extern "C" int rt_hostsim_fast_queries(rt_context* c, const float* rays, int n, float* out_t, int* out_k)
+{
+    if (!c || n < 0 || (n > 0 && (!rays || !out_t || !out_k))) return RT_ERR_ARG;
+    if (!c->have_bvh) return RT_ERR_STATE;
+    const RtSceneView S = rt_host_view(c);
+#pragma omp parallel
+    {
+        rtk::IdxStack<RT_HOSTSIM_FAST_CAP> fst;
+#pragma omp for schedule(dynamic, 64)
+        for (int i = 0; i < n; i++) {
+            const float* r = rays + 6 * (size_t)i;
+            float t;
+            int k;
+            if (rtk::fast_query_closest(S, rtk::v3(r[0], r[1], r[2]), rtk::v3(r[3], r[4], r[5]), fst, t, k, nullptr)) {
+                out_t[i] = t;
+                out_k[i] = k < 0 ? -1 : (int)rt_asuint(S.tri4[3 * (size_t)k].w);
+            } else {
+                out_t[i] = -2.0f;
+                out_k[i] = -2;
+            }
+        }
+    }
+    return RT_OK;
+}
+
 // Heap-order emulation self-check against std::priority_queue (exported for
 // tests/test_hostsim.py): keys[m] in push order -> order[m] of pushed indices.
 #include <queue>

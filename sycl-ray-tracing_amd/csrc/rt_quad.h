@@ -389,35 +389,37 @@ __device__ __forceinline__ int quad_visit(const RtSceneView& S, QState& q, QSTK&
                 }
             }
         } else {
-            float m1 = tv, m2 = __builtin_inff();
-            {
-                const float o1 = qdppf<RT_QX1>(m1), o2 = qdppf<RT_QX1>(m2);
-                const float n1 = __builtin_fminf(m1, o1), n2 = __builtin_fminf(__builtin_fmaxf(m1, o1), __builtin_fminf(m2, o2));
-                m1 = n1, m2 = n2;
-            }
-            {
-                const float o1 = qdppf<RT_QX2>(m1), o2 = qdppf<RT_QX2>(m2);
-                const float n1 = __builtin_fminf(m1, o1), n2 = __builtin_fminf(__builtin_fmaxf(m1, o1), __builtin_fminf(m2, o2));
-                m1 = n1, m2 = n2;
-            }
-            int pm = tv == m1 ? prim : 0x7fffffff;
-            pm = min(pm, qdpp<RT_QX1>(pm));
-            pm = min(pm, qdpp<RT_QX2>(pm));
-            const bool mine = tv == m1 && prim == pm;
+            // rt_fast.h fast_take over the quad's four hits: m1 the closest, m2 the next distance
+            // above it, the winner among the lanes at m1 (brute force: lowest original index;
+            // else lowest leaf-order k, the first in its octree leaf's list), and whether the
+            // lanes at m1 span more than one octree leaf (a tie only the exact walk settles)
+            float m1 = __builtin_fminf(tv, qdppf<RT_QX1>(tv));
+            m1 = __builtin_fminf(m1, qdppf<RT_QX2>(m1));
+            float m2 = tv > m1 ? tv : __builtin_inff();
+            m2 = __builtin_fminf(m2, qdppf<RT_QX1>(m2));
+            m2 = __builtin_fminf(m2, qdppf<RT_QX2>(m2));
+            int key = tv == m1 ? (S.brute ? prim : k) : 0x7fffffff;
+            key = min(key, qdpp<RT_QX1>(key));
+            key = min(key, qdpp<RT_QX2>(key));
+            const bool mine = tv == m1 && (S.brute ? prim : k) == key;
+            const int wk = qor(mine ? k : 0), wl = qor(mine ? leaf : 0), wp = qor(mine ? prim : 0);
+            const bool mixed = qor(tv == m1 && m1 < __builtin_inff() && leaf != wl ? 1 : 0) != 0;
             if (m1 < h.t) {
                 h.t2 = __builtin_fminf(h.t, m2);
                 h.t = m1;
-                h.k = qor(mine ? k : 0);
-                h.leaf = qor(mine ? leaf : 0);
-                h.prim = pm;
-                h.tie = m2 == m1;
+                h.k = wk;
+                h.leaf = wl;
+                h.prim = wp;
+                h.tie = mixed;
             } else if (m1 == h.t && m1 < __builtin_inff()) {
-                h.tie = true;
-                h.t2 = m1;
-                if (pm < h.prim) {
-                    h.k = qor(mine ? k : 0);
-                    h.leaf = qor(mine ? leaf : 0);
-                    h.prim = pm;
+                h.t2 = __builtin_fminf(h.t2, m2);
+                if (S.brute) {
+                    h.tie = true;
+                    if (wp < h.prim) h.k = wk, h.leaf = wl, h.prim = wp;
+                } else if (!mixed && wl == h.leaf) {
+                    if (wk < h.k) h.k = wk, h.prim = wp;
+                } else {
+                    h.tie = true;
                 }
             } else {
                 h.t2 = __builtin_fminf(h.t2, m1);

@@ -773,6 +773,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_STEP_OCC
 __device__ __noinline__ void walk_log(const rtk::WaveView& W, rtk::V3 o, rtk::V3 d, uint32_t target, int calls, float t,
                                       int k, int where)
 {
+    if (W.wlog_every < 0 && t != -2.0f) return;  // (only the walks left to the exact walk)
     if (W.wlog_every > 1 && ((target * 2654435761u) ^ ((uint32_t)W.iter * 40503u)) % (uint32_t)W.wlog_every != 0u) return;
     const int i = atomicAdd(W.wlog_n, 1);
     if (i >= W.wlog_cap) return;
@@ -841,11 +842,15 @@ __device__ __forceinline__ void trace_stream(const rtk::WaveView& W, const RtSce
         }
         float t = 0.0f;
         int k = 0;
+        int why = res < 0 ? 3 : 0;  // (walk log: why the exact walk answers: 1 tie, 2 chain check, 3 stack overflow)
         // (rows: each quad of the row verifies alike; one counts)
-        if (res > 0 && !ANY && !rtk::quad_closest_answer(S, q, sub & 3, t, k, gs == 4 || sub == 0 ? ps : nullptr))
+        if (res > 0 && !ANY && !rtk::quad_closest_answer(S, q, sub & 3, t, k, gs == 4 || sub == 0 ? ps : nullptr)) {
             res = -1;
+            why = q.h.tie ? 1 : 2;
+        }
         if (STATS && W.wlog && sub == 0 && q.calls >= W.wlog_min)
-            walk_log(W, q.o, q.d, target, q.calls, res <= 0 ? -2.0f : ANY ? (float)(q.h.k == 1) : t, k, gs == 4 ? 0 : 1);
+            walk_log(W, q.o, q.d, target, q.calls, res <= 0 ? -2.0f : ANY ? (float)(q.h.k == 1) : t, res <= 0 ? why : k,
+                     gs == 4 ? 0 : 1);
         if (sub == 0) {
             if (res > 0) {
                 if (ANY)

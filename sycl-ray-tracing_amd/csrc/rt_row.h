@@ -63,15 +63,14 @@ __device__ __forceinline__ int row_min(int v)
     v = min(v, rdpp<RT_DPP_ROW_HALF_MIRROR>(v));
     return min(v, rdpp<RT_DPP_ROW_MIRROR>(v));
 }
-// (closest, second) pairs merged over the row
-template <int CTRL>
-__device__ __forceinline__ void row_merge2(float& m1, float& m2)
+// minimum over the row's 16 lanes (every lane gets it)
+__device__ __forceinline__ float row_minf(float v)
 {
-    const float o1 = rdppf<CTRL>(m1), o2 = rdppf<CTRL>(m2);
-    const float n1 = __builtin_fminf(m1, o1), n2 = __builtin_fminf(__builtin_fmaxf(m1, o1), __builtin_fminf(m2, o2));
-    m1 = n1, m2 = n2;
+    v = __builtin_fminf(v, qdppf<RT_QX1>(v));
+    v = __builtin_fminf(v, qdppf<RT_QX2>(v));
+    v = __builtin_fminf(v, rdppf<RT_DPP_ROW_HALF_MIRROR>(v));
+    return __builtin_fminf(v, rdppf<RT_DPP_ROW_MIRROR>(v));
 }
-
 // Rank of (key, lane) among the row's 16 pairs: a permutation of 0..15 (the lane
 // each rotation reads from is taken from the rotation itself, not assumed).
 template <int K>
@@ -192,27 +191,29 @@ __device__ __forceinline__ int row_visit(const RtSceneView& S, QState& q, RSTK& 
                 }
             }
         } else {
-            float m1 = tv, m2 = __builtin_inff();
-            row_merge2<RT_QX1>(m1, m2);
-            row_merge2<RT_QX2>(m1, m2);
-            row_merge2<RT_DPP_ROW_HALF_MIRROR>(m1, m2);
-            row_merge2<RT_DPP_ROW_MIRROR>(m1, m2);
-            const int pm = row_min(tv == m1 ? prim : 0x7fffffff);
-            const bool mine = tv == m1 && prim == pm;
+            // rt_quad.h's leaf reduction over the row's sixteen hits (rt_fast.h fast_take)
+            const float m1 = row_minf(tv);
+            const float m2 = row_minf(tv > m1 ? tv : __builtin_inff());
+            const int key = row_min(tv == m1 ? (S.brute ? prim : k) : 0x7fffffff);
+            const bool mine = tv == m1 && (S.brute ? prim : k) == key;
+            const int wk = row_or(mine ? k : 0), wl = row_or(mine ? leaf : 0), wp = row_or(mine ? prim : 0);
+            const bool mixed = row_or(tv == m1 && m1 < __builtin_inff() && leaf != wl ? 1 : 0) != 0;
             if (m1 < h.t) {
                 h.t2 = __builtin_fminf(h.t, m2);
                 h.t = m1;
-                h.k = row_or(mine ? k : 0);
-                h.leaf = row_or(mine ? leaf : 0);
-                h.prim = pm;
-                h.tie = m2 == m1;
+                h.k = wk;
+                h.leaf = wl;
+                h.prim = wp;
+                h.tie = mixed;
             } else if (m1 == h.t && m1 < __builtin_inff()) {
-                h.tie = true;
-                h.t2 = m1;
-                if (pm < h.prim) {
-                    h.k = row_or(mine ? k : 0);
-                    h.leaf = row_or(mine ? leaf : 0);
-                    h.prim = pm;
+                h.t2 = __builtin_fminf(h.t2, m2);
+                if (S.brute) {
+                    h.tie = true;
+                    if (wp < h.prim) h.k = wk, h.leaf = wl, h.prim = wp;
+                } else if (!mixed && wl == h.leaf) {
+                    if (wk < h.k) h.k = wk, h.prim = wp;
+                } else {
+                    h.tie = true;
                 }
             } else {
                 h.t2 = __builtin_fminf(h.t2, m1);

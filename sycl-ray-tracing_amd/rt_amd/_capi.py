@@ -86,6 +86,7 @@ _SIGS = {
     "rt_device_queries": (I, [P, I, P, I, I, P, P, P]),
     # hostsim-only extra
     "rt_hostsim_heap_order": (I, [P, I, P, P]),
+    "rt_hostsim_fast_queries": (I, [P, P, I, P, P]),
 }
 
 STAT_NAMES = ["rays", "vol", "tri", "leaf", "mat", "env", "cdf", "heap_slow", "any_rays", "any_vol", "any_tri",

@@ -200,3 +200,31 @@ def test_hostsim_tiny_scenes_match_oracle(n, cameras):
     """Empty scene (sky only), one and two triangles, five (one leaf split)."""
     got, want = rt_cases.render_tiny(n, cameras, hostsim=True)
     assert gio.compare_rgb(got, want)["bitwise_fraction"] == 1.0
+
+
+@pytest.mark.parametrize("fixture", ["rays_dragon.npz", "brute_rays_dragon_tie_prone.npz"])
+def test_fast_walk_settles_same_leaf_ties_like_the_octree_walk(fixture):
+    """The search-BVH walk's answer (rt_fast.h fast_query_closest, the k_trace stage) on
+    tie-prone rays (rays through triangle edges and vertices of the reference-pinned
+    fixtures): every ray it settles, including two triangles hit at exactly the same t inside
+    one octree leaf (the first in that leaf's list wins, bvh.h:150-161), gives the exact octree
+    walk's (t, triangle); only ties across leaves (and failed chain checks) are left to the
+    exact walk."""
+    P = parsed_scene("dragon")
+    rk = rt_amd.RenderKernel(4, 4, 1, 1, rt_amd.Image(4, 4), P.triangles, P.materials, P.emissive_triangle_indices,
+                             P.material_indices, None, rt_amd.BVH(P.triangles),
+                             rt_amd.Image.from_rgb(np.ones((8, 16, 3), np.float32)), None, hostsim=True)
+    g = load_golden(fixture)
+    rays = np.ascontiguousarray((g["rays"] if "rays" in g else g[list(g.keys())[0]])[:, :6], dtype=np.float32)
+    n = rays.shape[0]
+    t = np.zeros(n, np.float32)
+    k = np.zeros(n, np.int32)
+    L = _capi.lib(hostsim=True)
+    assert L.rt_hostsim_fast_queries(rk.ctx, _capi.ptr(rays), n, _capi.ptr(t), _capi.ptr(k)) == 0
+    ex = rk.intersect(rays)
+    ok = t != -2.0
+    want_t = np.where(ex[:, 0] == 1, ex[:, 2].view(np.float32), -1.0).astype(np.float32)
+    np.testing.assert_array_equal(t[ok].view(np.uint32), want_t[ok].view(np.uint32))
+    hit = ok & (ex[:, 0] == 1)
+    np.testing.assert_array_equal(k[hit], ex[hit, 1])
+    assert ok.mean() > 0.95, f"{(~ok).sum()} of {n} left to the exact walk"

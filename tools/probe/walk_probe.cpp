@@ -638,14 +638,27 @@ int main(int argc, char** argv)
             tr = product_tree(fb);
             if (v != "product") add_slabs(tr, T, v.size() > 12 && v[12] == ':' ? std::stof(v.substr(13)) : 0.5f);
         } else {
+            // "sah" / "sbvh[:alpha]" / "sah:16", or key=value tokens after a comma:
+            // bins=N, leaf=N, alpha=X, slab (add slabs, align 0.5), slab=ALIGN
             Builder B(T);
-            const size_t c = v.find(':');
-            const std::string kind = v.substr(0, c);
+            std::string head = v.substr(0, v.find(','));
+            const size_t c = head.find(':');
+            const std::string kind = head.substr(0, c);
             if (kind == "sbvh") {
                 B.spatial = true;
-                if (c != std::string::npos) B.alpha = std::stof(v.substr(c + 1));
+                if (c != std::string::npos) B.alpha = std::stof(head.substr(c + 1));
             } else if (c != std::string::npos) {
-                B.bins = std::stoi(v.substr(c + 1));
+                B.bins = std::stoi(head.substr(c + 1));
+            }
+            float slab_align = -1.0f;
+            for (size_t p = v.find(','); p != std::string::npos; p = v.find(',', p + 1)) {
+                const std::string tok = v.substr(p + 1, v.find(',', p + 1) - p - 1);
+                const size_t eq = tok.find('=');
+                const std::string key = tok.substr(0, eq), val = eq == std::string::npos ? "" : tok.substr(eq + 1);
+                if (key == "bins") B.bins = std::stoi(val);
+                else if (key == "leaf") B.leaf_max = std::stoi(val);
+                else if (key == "alpha") B.alpha = std::stof(val);
+                else if (key == "slab") slab_align = val.empty() ? 0.5f : std::stof(val);
             }
             std::vector<Ref> R(nt);
             for (int i = 0; i < nt; i++) {
@@ -657,6 +670,7 @@ int main(int argc, char** argv)
             tr = B.collapse();
             nrefs = (long)B.leaf_refs.size();
             splits = B.splits;
+            if (slab_align >= 0) add_slabs(tr, T, slab_align);
         }
         tr.build_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
         std::vector<int> trips[2], all;

@@ -93,6 +93,11 @@ def analyse(log: np.ndarray, total: int, min_calls: int) -> dict:
     slots, counts = np.unique(log["slot"], return_counts=True)
     res["distinct_paths"] = int(slots.size)
     res["walks_per_path_quantiles"] = {q: int(np.quantile(counts, q)) for q in (0.5, 0.9, 0.99, 1.0)} if n else {}
+    fbk = log["t"] == -2
+    if fbk.any():  # walks left to the exact walk: their triangle field says why
+        res["exact_walk_reasons"] = {name: {KINDS[k]: int((fbk & (log["tri"] == code) & (log["kind"] == k)).sum())
+                                            for k in range(6) if (fbk & (log["tri"] == code) & (log["kind"] == k)).any()}
+                                     for code, name in ((1, "tie"), (2, "chain_check"), (3, "stack_overflow"))}
     it = log["iter"]
     res["by_iteration_band"] = {f"{a}-{b - 1}": int(((it >= a) & (it < b)).sum())
                                 for a, b in zip([0, 100, 200, 300, 400, 500, 600, 800], [100, 200, 300, 400, 500, 600, 800, 1 << 20])}
@@ -106,7 +111,7 @@ def main():
     ap.add_argument("--rank", type=int, default=1)
     ap.add_argument("--min-calls", type=int, default=24)
     ap.add_argument("--capacity", type=int, default=4 << 20)
-    ap.add_argument("--sample-every", type=int, default=1, help="keep every k-th walk by a hash (all walks: --min-calls 1)")
+    ap.add_argument("--sample-every", type=int, default=1, help="keep every k-th walk by a hash (all walks: --min-calls 1); -1: only the walks left to the exact walk")
     ap.add_argument("--out", default=os.path.join(REPO, "gpurun_out", "walk_attrib"))
     args = ap.parse_args()
     import torch
