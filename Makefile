@@ -63,6 +63,11 @@ build/cdf_check: tests/native/cdf_check.cpp $(OBJ)/rt_scene.host.o $(HDRS)
 	@mkdir -p build
 	$(CXX) $(CXXFLAGS) -I$(SRC) $< $(OBJ)/rt_scene.host.o -o $@
 
+# CPU replay of logged rays over search-BVH variants (tools/probe/walk_probe.cpp; study tool)
+build/walk_probe: tools/probe/walk_probe.cpp $(OBJ)/rt_scene.host.o $(HDRS)
+	@mkdir -p build
+	$(CXX) -std=c++17 -O2 -fopenmp -ffp-contract=off -I$(SRC) $< $(OBJ)/rt_scene.host.o -o $@ -lpthread
+
 # the reference build (container only; needs /root/reference)
 ref:
 	$(MAKE) -C oracle/ref OPT=-O2

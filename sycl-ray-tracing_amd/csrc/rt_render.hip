@@ -1339,7 +1339,7 @@ __global__ __launch_bounds__(256, 4) void k_query(RtSceneView S, const float4_* 
             int k = 0;
             const bool ok = rtk::fast_query_closest<decltype(stk), WALK>(S, o, d, stk, t, k, nullptr);
             out_t[i] = ok ? t : -2.0f;
-            out_k[i] = ok ? k : -2;
+            out_k[i] = ok ? (k >= 0 ? (int)rt_asuint(S.tri4[3 * (size_t)k].w) : -1) : -2;  // (the original triangle index)
         }
     }
 }
@@ -1370,7 +1370,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
                 out_k[i] = 0;
             } else {
                 out_t[i] = ok ? t : -2.0f;
-                out_k[i] = ok ? k : -2;
+                out_k[i] = ok ? (k >= 0 ? (int)rt_asuint(S.tri4[3 * (size_t)k].w) : -1) : -2;  // (the original triangle index)
             }
         }
     }
@@ -1401,7 +1401,7 @@ __global__ __launch_bounds__(256) void k_query_row(RtSceneView S, const float4_*
                 out_k[i] = 0;
             } else {
                 out_t[i] = ok ? t : -2.0f;
-                out_k[i] = ok ? k : -2;
+                out_k[i] = ok ? (k >= 0 ? (int)rt_asuint(S.tri4[3 * (size_t)k].w) : -1) : -2;  // (the original triangle index)
             }
         }
     }
