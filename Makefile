@@ -95,6 +95,15 @@ build/shim_test: tests/native/shim_test.cpp include/render_kernel_hip.h include/
 	  $(REFOBJ)/mat.o $(REFOBJ)/camera.o $(REFOBJ)/ray.o $(REFOBJ)/utils.o -Wl,--gc-sections \
 	  -L$(LIB) -lrt_hostsim -Wl,-rpath,'$$ORIGIN/../$(LIB)' -o $@
 
+# the same drop-in linked to the product library (gfx950): built here, run on the GPU box by
+# tests/test_shim.py's gpu test (the box has no /root/reference; the binary carries what it needs)
+build/shim_test_hip: tests/native/shim_test.cpp include/render_kernel_hip.h include/rt_hip.h $(LIB)/librt_hip.so
+	@mkdir -p build
+	$(CXX) -std=gnu++20 -O2 -fopenmp -Iinclude -I$(REFDIR)/include -I$(REFDIR)/rapidobj -I$(REFDIR) $< \
+	  $(REFOBJ)/bvh.o $(REFOBJ)/flattened_bvh.o $(REFOBJ)/triangle.o $(REFOBJ)/vec.o $(REFOBJ)/color.o \
+	  $(REFOBJ)/mat.o $(REFOBJ)/camera.o $(REFOBJ)/ray.o $(REFOBJ)/utils.o -Wl,--gc-sections \
+	  -L$(LIB) -lrt_hip -Wl,-rpath,'$$ORIGIN/../$(LIB)' -o $@
+
 # Host sanitizers: the hostsim build of the render path + the CPU oracle +
 # tests/native/sanitize_driver.cpp in one executable per sanitizer.
 #   make sanitize  -> build/sanitize_asan (ASan + UBSan) and build/sanitize_tsan (TSan), run

@@ -191,6 +191,8 @@ int rt_test_schedule(rt_context* c, const char* key, double value)
     else if (k == "tail_spec_cam") s.tail_spec_cam = std::min(2, v);
     else if (k == "force_fallback") s.force_fallback = std::max(0, v);
     else if (k == "step_budget") s.step_budget = v;
+    else if (k == "fast_k") s.fast_k = v;
+    else if (k == "fast_spp") s.fast_spp = value;
     else if (k == "reset") s = RtSchedule{};
     else return rt_fail(c, RT_ERR_ARG, "rt_test_schedule: unknown key " + k);
     return RT_OK;

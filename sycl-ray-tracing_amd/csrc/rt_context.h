@@ -30,6 +30,8 @@ struct RtSchedule {
     int tail_spec_cam = -1;    // the same in k_tail
     int force_fallback = 0;    // stressor: every k-th query (by a ray hash) skips to the exact walk
     int step_budget = -1;      // exact-walk steps per query per launch before it parks
+    int fast_k = -1;           // fast lane: this many of the slowest paths to a tail kernel early (0: off)
+    double fast_spp = -1.0;    // ... at the lanes' first readback from iteration fast_spp x spp on
 };
 
 // Diagnostics, read from the environment once when the context is created (rt_create*):

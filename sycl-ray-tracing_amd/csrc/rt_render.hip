@@ -50,6 +50,9 @@ namespace {
 
 #define RT_MAX_TIMED_ITERS 16384
 #define RT_MAX_LANES 4  // wavefront lanes (streams) per render (run_wave)
+#define RT_FAST_K 768         // fast lane: paths handed over (run_wave)
+#define RT_FAST_SPP 2.25      // ... from iteration RT_FAST_SPP x spp on
+#define RT_FAST_MAX_SPP 4096  // ... in renders of at most this many samples per pixel
 #define RT_LANES4_MAX 1572864  // auto lanes: 4 at most this many slots per launch, else 3
 #ifndef RT_STEP_OCC
 #define RT_STEP_OCC 3  // k_step waves per SIMD
@@ -163,6 +166,14 @@ struct Backend {
     DevBuf wlog;      // stats renders with a walk log: count (256 B), then 3 float4 per record
     DevBuf wave[RT_MAX_LANES];      // per lane: path state, pending records, results, queues, lists
     DevBuf counters[RT_MAX_LANES];  // per lane: C_COUNT int32
+    // fast lane (rt_test_schedule fast_k): per lane its handed-over list + ticket, counters,
+    // samples-done histogram and spill area; the lanes' views for the one tail kernel over them
+    DevBuf fast[RT_MAX_LANES], fcnt[RT_MAX_LANES], fhist[RT_MAX_LANES], fspill[RT_MAX_LANES], fviews;
+    int32_t* h_hist[RT_MAX_LANES] = {};
+    rtk::WaveView* h_fviews = nullptr;  // pinned
+    hipEvent_t fev[RT_MAX_LANES] = {}, fev_done = nullptr;
+    bool fev_done_recorded = false;
+    hipStream_t fs = nullptr;  // the fast lane's stream with 4 lanes (fewer: the first idle lane stream)
     DevBuf xy;        // pixel list (rt_render_pixels)
     DevBuf fb;        // host-fb staging
     int32_t* h_act[RT_MAX_LANES] = {};     // per lane, pinned: live-slot counters (sharded) + 8 fallback counters
@@ -768,6 +779,39 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_STEP_OCC
     flush_stats<STATS>(st, stats);
 }
 
+// The fast lane's hand-over (run_wave), between a lane's k_trace and k_step: the live paths of
+// iteration par's list with at most W.fast_thr samples done and no parked query, up to
+// W.fast_cap of them, move to W.fast_list (their wait counts become -1: k_step drops them from
+// the lane's live list, rt_wave.h path_step; the fast lane's tail kernel clears the mark).
+__global__ __launch_bounds__(256) void k_hand(rtk::WaveView W, int par)
+{
+    __shared__ int s_pre[RT_QSHARDS + 1];
+    shard_prefix(W.counters, RT_QSHARDS, [&](int j) { return ac_at(par, j); }, s_pre);
+    const int n = s_pre[RT_QSHARDS];
+    for (int idx = (int)(blockIdx.x * blockDim.x + threadIdx.x); idx < n; idx += (int)(gridDim.x * blockDim.x)) {
+        const int sh = shard_find(s_pre, RT_QSHARDS, idx);
+        const int p = W.act_in[(size_t)sh * W.seg_cap + (idx - s_pre[sh])];
+        if ((int)rt_asuint(W.p_thr[p].w) > W.fast_thr || W.r_park[p] != 0) continue;
+        const int j = atomicAdd(W.fast_ticket, 1);
+        if (j >= W.fast_cap) continue;
+        W.fast_list[j] = p;
+        W.r_park[p] = -1;
+    }
+}
+
+// Samples done by the live paths of iteration par's list (the fast lane's selection, run_wave).
+__global__ __launch_bounds__(256) void k_hist(rtk::WaveView W, int par, int32_t* __restrict__ hist)
+{
+    __shared__ int s_pre[RT_QSHARDS + 1];
+    shard_prefix(W.counters, RT_QSHARDS, [&](int j) { return ac_at(par, j); }, s_pre);
+    const int n = s_pre[RT_QSHARDS];
+    for (int idx = (int)(blockIdx.x * blockDim.x + threadIdx.x); idx < n; idx += (int)(gridDim.x * blockDim.x)) {
+        const int sh = shard_find(s_pre, RT_QSHARDS, idx);
+        const int p = W.act_in[(size_t)sh * W.seg_cap + (idx - s_pre[sh])];
+        atomicAdd(hist + min((int)rt_asuint(W.p_thr[p].w), W.spp), 1);
+    }
+}
+
 // Stats renders with a walk log (rt_test_walk_log, include/rt_hip.h): one record per walk of at
 // least W.wlog_min quad_visit calls. where: 0 k_trace quads, 1 a k_trace drain's rows, 2 k_tail.
 __device__ __noinline__ void walk_log(const rtk::WaveView& W, rtk::V3 o, rtk::V3 d, uint32_t target, int calls, float t,
@@ -1118,8 +1162,11 @@ __device__ __noinline__ void tail_exact(const rtk::WaveView& W, int l, uint32_t 
 #ifndef RT_TAIL_OCC
 #define RT_TAIL_OCC 3    // k_tail waves per SIMD (2: no spills but half the paths per launch; 3 measured faster)
 #endif
-template <bool STATS, bool PAIR = true, int G = 4>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TAIL_OCC, RT_TAIL_OCC))) void k_tail(rtk::WaveView W, int par, unsigned long long* stats)
+// FAST: the fast lane's launch, one kernel over every lane's handed-over paths: blocks
+// [fparts[l], fparts[l + 1]) step lane l's (fviews[l]: its fast list as shard 0 of its own
+// counters, its own spill area).
+template <bool STATS, bool PAIR, int G, bool FAST>
+__device__ __forceinline__ void tail_body(const rtk::WaveView& W, int par, unsigned long long* stats, int blk)
 {
     __shared__ rtk::RayRec s_q[4][2][RT_TAIL_MAXP * rtk::RK_COUNT];  // per wave: closest list, occlusion list
     __shared__ uint32_t s_stk[2 * RT_QSTACK * 64];
@@ -1128,7 +1175,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TAIL_OCC
     rtk::lds_shade_init(W.S);  // (the env-map row search and a small material table from LDS)
     int32_t* cnt = W.counters;
     shard_prefix(cnt, RT_QSHARDS, [&](int j) { return ac_at(par, j); }, s_pre);
-    const int n = s_pre[RT_QSHARDS];
+    const int n = FAST ? min(s_pre[RT_QSHARDS], W.fast_cap) : s_pre[RT_QSHARDS];  // (fast lane: its list)
     const RtSceneView S = W.S;
     rtk::Stats st;
     if (STATS)
@@ -1141,7 +1188,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TAIL_OCC
     const int wv = (int)(threadIdx.x >> 6), lane = lane_id(), sub = lane & (G - 1), qd = (int)(threadIdx.x / G);
     using STK = rtk::QuadStack<SCAP, GPB>;
     STK stk{s_stk + qd, (float*)s_stk + SCAP * GPB + qd};
-    const size_t gl = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const size_t gl = (size_t)blk * blockDim.x + threadIdx.x;
     rtk::SpillStack<STK> xs{stk, W.spill_r + gl * RT_STACK_CAP, W.spill_k + gl * RT_STACK_CAP};
     const int P = W.tail_paths;
     const int last_kind = W.any_rays ? rtk::RK_CAM : rtk::RK_BENV;
@@ -1166,6 +1213,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TAIL_OCC
             if (need && idx < n) {
                 const int sh = shard_find(s_pre, RT_QSHARDS, idx);
                 my = W.act_in[(size_t)sh * W.seg_cap + (idx - s_pre[sh])];
+                if (FAST) W.r_park[my] = 0;  // (k_hand's mark)
             }
         }
         if (!__any(my >= 0)) break;
@@ -1285,6 +1333,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TAIL_OCC
     }
     flush_stats<STATS>(st, stats);
     flush_stats<STATS>(st, stats + RT_STAT_COUNT);  // (the tail kernel's share, for per-kernel byte counts)
+}
+template <bool STATS, bool PAIR = true, int G = 4>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TAIL_OCC, RT_TAIL_OCC))) void k_tail(
+    rtk::WaveView W, int par, unsigned long long* stats)
+{
+    tail_body<STATS, PAIR, G, false>(W, par, stats, (int)blockIdx.x);
+}
+template <bool STATS, bool PAIR = true, int G = 4>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TAIL_OCC, RT_TAIL_OCC))) void k_tail_fast(
+    const rtk::WaveView* __restrict__ fviews, int4 fparts, unsigned long long* stats)
+{
+    const int b = (int)blockIdx.x;
+    const int fl = (b >= fparts.y) + (b >= fparts.z) + (b >= fparts.w);
+    const int b0 = fl == 0 ? 0 : fl == 1 ? fparts.y : fl == 2 ? fparts.z : fparts.w;
+    tail_body<STATS, PAIR, G, true>(fviews[fl], 0, stats, b - b0);
 }
 
 __global__ __launch_bounds__(256) void k_intersect(RtSceneView S, const float* __restrict__ rays, int32_t* __restrict__ out,
@@ -1530,12 +1593,19 @@ void destroy_one(Backend* b)
     (void)hipDeviceSynchronize();
     DevBuf* all[] = {&b->nodes, &b->tri4, &b->prim2k, &b->mat_idx, &b->mats, &b->emissive, &b->spheres, &b->env,
                      &b->env_lum, &b->cdf, &b->bvh4, &b->bvh16, &b->bvh4s, &b->bvh16s, &b->bvh_tri4, &b->parent, &b->leaf_of, &b->cdf_row, &b->cdf_coarse,
-                     &b->cdf_fence, &b->matk, &b->stats, &b->xy, &b->fb, &b->iterq, &b->wlog};
+                     &b->cdf_fence, &b->matk, &b->stats, &b->xy, &b->fb, &b->iterq, &b->wlog, &b->fviews};
     for (DevBuf* d : all)
         if (d->p) (void)hipFree(d->p);
     for (int l = 0; l < RT_MAX_LANES; l++)
-        for (DevBuf* d : {&b->wave[l], &b->counters[l]})
+        for (DevBuf* d : {&b->wave[l], &b->counters[l], &b->fast[l], &b->fcnt[l], &b->fhist[l], &b->fspill[l]})
             if (d->p) (void)hipFree(d->p);
+    for (int l = 0; l < RT_MAX_LANES; l++) {
+        if (b->h_hist[l]) (void)hipHostFree(b->h_hist[l]);
+        if (b->fev[l]) (void)hipEventDestroy(b->fev[l]);
+    }
+    if (b->h_fviews) (void)hipHostFree(b->h_fviews);
+    if (b->fev_done) (void)hipEventDestroy(b->fev_done);
+    if (b->fs) (void)hipStreamDestroy(b->fs);
     for (int l = 0; l < RT_MAX_LANES; l++) {
         if (b->h_act[l]) (void)hipHostFree(b->h_act[l]);
         if (b->ev_lane[l]) (void)hipEventDestroy(b->ev_lane[l]);
@@ -1713,6 +1783,8 @@ struct WaveLane {
     long live = 0;  // live paths at the last readback (an upper bound: paths only finish)
     bool done = false, tail_next = false;
     int await = 0;  // 0 none, 1 live count, 2 fallback counts (tail entry check)
+    int fast_state = 0;  // fast lane: 0 waiting, 1 hand-over at the next k_step, 2 handed over, 3 none
+    int fast_thr = 0, fast_n = 0;  // ... samples-done threshold, paths at most
     hipEvent_t (*tev)[RT_MAX_TIMED_ITERS] = nullptr;  // [3][RT_MAX_TIMED_ITERS]
 };
 
@@ -1751,7 +1823,9 @@ int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounces, cons
     }
     // lanes: rows interleave (row j of the launch -> lane j % lanes); pixel lists split in runs
     const int lanes_set = sc.lanes > 0 ? std::min(RT_MAX_LANES, sc.lanes) : b->lanes;
-    int nl = lanes_set > 0 ? lanes_set : n <= RT_LANES4_MAX ? 4 : 3;
+    const int fast_k = spp <= RT_FAST_MAX_SPP ? std::max(0, std::min(1 << 16, sc.fast_k >= 0 ? sc.fast_k : RT_FAST_K)) : 0;
+    // (auto: 3 lanes with the fast lane, the fourth hardware queue its stream)
+    int nl = lanes_set > 0 ? lanes_set : n <= RT_LANES4_MAX && fast_k == 0 ? 4 : 3;
     const int rows = src.xy ? 0 : n / src.W;
     while (nl > 1 && (n < nl * 65536 || (!src.xy && rows < nl))) nl--;
     WaveLane L[RT_MAX_LANES];
@@ -1788,6 +1862,19 @@ int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounces, cons
     // one MI355X: 2.0 / 1.5 / 1.25 / 1.0 -> 384-391 / 380-384 / 379-383 / 382-390 ms,
     // profiles/r03_tail_enter4.json)
     const double tail_enter = sc.tail_enter >= 0.0 ? sc.tail_enter : nl == 4 ? 1.4 : 2.0;
+    // Fast lane: from iteration fast_spp x spp on, each lane's share of the fast_k live paths
+    // with the fewest samples done (the pixels with the longest chains, tools/fastlane_model.py)
+    // leaves the wavefront at the lane's next k_step; when every lane has handed its share over,
+    // one tail kernel steps them all on a stream of their own (an idle lane's: 3 lanes + the fast
+    // lane are the 4 hardware queues), at a tail round's pace beside the wavefront. cfg4 8-way
+    // shard (rank 1) / cfg2, one MI355X, 3 rounds (profiles/r05_fast_lane.json): 4 lanes, none
+    // 319.7-323.9 / 134.9-135.4 ms; 3 lanes + fast lane 768 paths at 2.0 / 2.25 x spp
+    // 311.5-316.1 / 134.7-136.4 and 312.2-316.9 / 133.7-134.0; 1024 paths 308.1-317.6; 1536 and
+    // more slower (r04's fast lane beside 4 lanes, a fifth stream: slower, r04x).
+    const long fast_iter = (long)((sc.fast_spp >= 0.0 ? sc.fast_spp : RT_FAST_SPP) * spp);
+    bool fast_launched = false, fast_ran = false;
+    if (fast_k > 0 && nl == RT_MAX_LANES && !b->fs) HIPCHK(c, hipStreamCreateWithFlags(&b->fs, hipStreamNonBlocking));
+    const hipStream_t fstream = fast_k > 0 ? (nl < RT_MAX_LANES ? b->ls[nl] : b->fs) : nullptr;
     const long tail_max = (long)(tail_enter * tail_blocks * 4 * tail_p / nl);
     if (nl > 1) {
         HIPCHK(c, hipEventRecord(b->ev_fork, s));
@@ -1847,6 +1934,18 @@ int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounces, cons
         W.tail_paths = tail_p;
         W.drain_rows = drain_rows;
         W.force_fb = force_fb;
+        W.fast_cap = 0;
+        La.fast_state = fast_k > 0 ? 0 : 3;
+        La.fast_n = (int)((long)fast_k * (l + 1) / nl - (long)fast_k * l / nl);
+        if (fast_k > 0) {  // the fast lane's buffers and events (first use)
+            if (int r = ensure(c, b->fast[l], (size_t)(La.fast_n + 1) * 4)) return r;
+            if (int r = ensure(c, b->fcnt[l], C_COUNT * sizeof(int32_t))) return r;
+            if (int r = ensure(c, b->fhist[l], (RT_FAST_MAX_SPP + 1) * 4)) return r;
+            if (int r = ensure(c, b->fspill[l], (size_t)((La.fast_n + 3) / 4) * threads * RT_STACK_CAP * 8)) return r;
+            if (!b->h_hist[l]) HIPCHK(c, hipHostMalloc((void**)&b->h_hist[l], (RT_FAST_MAX_SPP + 1) * 4, hipHostMallocDefault));
+            if (!b->fev[l]) HIPCHK(c, hipEventCreateWithFlags(&b->fev[l], hipEventDisableTiming));
+            HIPCHK(c, hipMemsetAsync(b->fcnt[l].p, 0, C_COUNT * sizeof(int32_t), La.s));
+        }
         W.iterq = (S && iter_log && l == 0) ? (int32_t*)b->iterq.p : nullptr;
         if (wlog) {
             W.wlog_n = (int32_t*)b->wlog.p;
@@ -1907,12 +2006,80 @@ int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounces, cons
         HIPCHK(c, hipGetLastError());
         return RT_OK;
     };
+    // the fast lane's tail kernel, once every lane has handed its share over (or has none)
+    auto fast_launch = [&]() -> int {
+        if (fast_k == 0 || fast_launched) return RT_OK;
+        bool any = false;
+        for (int l = 0; l < nl; l++) {
+            if (L[l].fast_state < 2) return RT_OK;
+            any = any || L[l].fast_state == 2;
+        }
+        fast_launched = true;
+        if (!any) return RT_OK;
+        if (!b->h_fviews)
+            HIPCHK(c, hipHostMalloc((void**)&b->h_fviews, sizeof(rtk::WaveView) * RT_MAX_LANES, hipHostMallocDefault));
+        if (!b->fev_done) HIPCHK(c, hipEventCreateWithFlags(&b->fev_done, hipEventDisableTiming));
+        if (b->fev_done_recorded) HIPCHK(c, hipEventSynchronize(b->fev_done));  // (the last render's copy of the views)
+        if (int r = ensure(c, b->fviews, sizeof(rtk::WaveView) * RT_MAX_LANES)) return r;
+        int start[RT_MAX_LANES + 1] = {}, tot = 0;
+        for (int l = 0; l < RT_MAX_LANES; l++) {
+            start[l] = tot;
+            if (l >= nl || L[l].fast_state != 2) continue;
+            rtk::WaveView FW = L[l].W;
+            FW.act_in = (int32_t*)b->fast[l].p;
+            FW.counters = (int32_t*)b->fcnt[l].p;
+            FW.fast_cap = L[l].fast_n;
+            FW.tail_paths = 1;  // (one path per wave, its queries on the wave's rows)
+            const int blocks = (L[l].fast_n + 3) / 4;
+            FW.spill_r = (uint32_t*)b->fspill[l].p;
+            FW.spill_k = (float*)((uint32_t*)b->fspill[l].p + (size_t)blocks * threads * RT_STACK_CAP);
+            FW.iterq = nullptr;
+            FW.spec_cam = spec_cam ? tail_spec_cam : 0;
+            b->h_fviews[l] = FW;
+            tot += blocks;
+            HIPCHK(c, hipStreamWaitEvent(fstream, b->fev[l], 0));
+        }
+        HIPCHK(c, hipMemcpyAsync(b->fviews.p, b->h_fviews, sizeof(rtk::WaveView) * RT_MAX_LANES, hipMemcpyHostToDevice,
+                                 fstream));
+        const rtk::WaveView* fv = (const rtk::WaveView*)b->fviews.p;
+        const int4 parts = make_int4(start[0], start[1], start[2], start[3]);
+        if (SEQ)
+            hipLaunchKernelGGL((k_tail_fast<true, false, 4>), dim3(tot), dim3(threads), 0, fstream, fv, parts, stats);
+        else if (S)
+            hipLaunchKernelGGL((k_tail_fast<true, true, 16>), dim3(tot), dim3(threads), 0, fstream, fv, parts, stats);
+        else
+            hipLaunchKernelGGL((k_tail_fast<false, true, 16>), dim3(tot), dim3(threads), 0, fstream, fv, parts, stats);
+        HIPCHK(c, hipGetLastError());
+        HIPCHK(c, hipEventRecord(b->fev_done, fstream));
+        b->fev_done_recorded = fast_ran = true;
+        return RT_OK;
+    };
     auto launch_step = [&](WaveLane& La) -> int {
         const int par = La.it & 1;
+        const int l = (int)(&La - L);
+        const bool hand = La.fast_state == 1;
+        int32_t* fl = (int32_t*)b->fast[l].p;
+        if (hand) {  // this step hands the lane's slowest paths to the fast lane
+            HIPCHK(c, hipMemsetAsync(fl + La.fast_n, 0, 4, La.s));
+            rtk::WaveView HW = La.W;
+            HW.fast_list = fl;
+            HW.fast_ticket = fl + La.fast_n;
+            HW.fast_cap = La.fast_n;
+            HW.fast_thr = La.fast_thr;
+            hipLaunchKernelGGL(k_hand, dim3((unsigned)std::min(1024l, (La.live + threads - 1) / threads)), dim3(threads), 0,
+                               La.s, HW, par);
+            HIPCHK(c, hipGetLastError());
+        }
         if (S)
             hipLaunchKernelGGL(k_step<true>, dim3(step_blocks_of(La)), dim3(threads), 0, La.s, La.W, par, stats);
         else
             hipLaunchKernelGGL(k_step<false>, dim3(step_blocks_of(La)), dim3(threads), 0, La.s, La.W, par, stats);
+        if (hand) {  // (its list's length as shard 0 of the fast lane's counters)
+            La.fast_state = 2;
+            HIPCHK(c, hipMemcpyAsync((int32_t*)b->fcnt[l].p + ac_at(0, 0), fl + La.fast_n, 4, hipMemcpyDeviceToDevice, La.s));
+            HIPCHK(c, hipEventRecord(b->fev[l], La.s));
+            if (int r = fast_launch()) return r;
+        }
         if (b->timing && La.it < RT_MAX_TIMED_ITERS) HIPCHK(c, hipEventRecord(La.tev[2][La.it], La.s));
         HIPCHK(c, hipGetLastError());
         La.it++;
@@ -1973,6 +2140,31 @@ int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounces, cons
         La.live = live;
         La.done = live == 0;
         La.tail_next = !La.done && live <= tail_max;
+        if (La.fast_state == 0 && (La.done || La.tail_next)) {  // (no hand-over from this lane)
+            La.fast_state = 3;
+            if (int r = fast_launch()) return r;
+        } else if (La.fast_state == 0 && La.it >= fast_iter) {
+            // the threshold: the samples-done count of the lane's fast_n-th slowest live path
+            const int l = (int)(&La - L);
+            int32_t* hh = (int32_t*)b->fhist[l].p;
+            HIPCHK(c, hipMemsetAsync(hh, 0, (size_t)(spp + 1) * 4, La.s));
+            rtk::WaveView HW = La.W;
+            HW.act_in = La.lists[La.it & 1];
+            hipLaunchKernelGGL(k_hist, dim3((unsigned)std::min(1024l, (live + threads - 1) / threads)), dim3(threads), 0,
+                               La.s, HW, La.it & 1, hh);
+            HIPCHK(c, hipGetLastError());
+            HIPCHK(c, hipMemcpyAsync(b->h_hist[l], hh, (size_t)(spp + 1) * 4, hipMemcpyDeviceToHost, La.s));
+            HIPCHK(c, hipStreamSynchronize(La.s));
+            long acc = 0;
+            int thr = spp;
+            for (int k = 0; k <= spp; k++)
+                if ((acc += b->h_hist[l][k]) >= La.fast_n) {
+                    thr = k;
+                    break;
+                }
+            La.fast_thr = thr;
+            La.fast_state = 1;
+        }
         return RT_OK;
     };
     for (int l = 0; l < nl; l++)
@@ -2018,6 +2210,8 @@ int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounces, cons
         }
     }
     for (int l = 0; l < nl; l++) {  // each lane's pixels tone-mapped after its last step
+        if (fast_ran)
+            HIPCHK(c, hipStreamWaitEvent(L[l].s, b->fev_done, 0));  // (and the fast lane's)
         hipLaunchKernelGGL(k_tonemap, dim3((L[l].n + threads - 1) / threads), dim3(threads), 0, L[l].s, L[l].W);
         HIPCHK(c, hipGetLastError());
     }

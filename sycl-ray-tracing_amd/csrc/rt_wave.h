@@ -128,6 +128,11 @@ struct WaveView {
     int iter;               // iteration of this launch
     int tail_paths;         // k_tail: paths per wave
     int drain_rows;         // k_trace: a wave's drain continues its walks as rows when at most this many remain
+    // fast lane (run_wave, rt_test_schedule fast_k): one k_step hands the live paths with at most
+    // fast_thr samples done (up to fast_cap of them) to the tail kernel on the fast stream
+    int32_t* fast_list;     // the handed-over slots
+    int32_t* fast_ticket;   // their count (may pass fast_cap: the tail kernel clamps)
+    int fast_cap, fast_thr; // fast_cap 0: off (k_tail: the list's length cap)
     int force_fb;           // test knob (RT_FORCE_FALLBACK): a query whose ray hashes to 0 mod force_fb
                             // skips the quad walk and takes the exact octree walk (0: off)
     int shards, seg_cap;    // queues and live lists: `shards` segments of seg_cap entries (device: rt_render.hip)
@@ -725,7 +730,10 @@ RT_HD void path_step(const WaveView& W, int p, Emit& e, Stats* st)
     const int cont_k = W.r_cont_k[p];
     const float cam_t = W.r_cam_t[p];  // (read only with PF_CAM)
     const int cam_k = W.r_cam_k[p];
-    if (park != 0) return;  // a query of this path is parked: wait
+    if (park != 0) {  // a query of this path is parked: wait (-1: handed to the fast lane, leaves the list)
+        e.active = park > 0;
+        return;
+    }
     if (st) st->c[RT_STAT_STEPS]++;
     if (heavy) {  // its last walk was long: this step's rays head the next streams
         e.heavy = true;

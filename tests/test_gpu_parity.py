@@ -268,20 +268,21 @@ def test_gpu_schedules_bit_identical():
     tail kernel on or off (1-8 paths per wave, entered at once or late), quad or
     row walks (rt_row.h) in the tail kernel and in k_trace, row
     shards split across lanes (framebuffer row pitch), k_trace's heavy class
-    (off, every walk heavy, the default) and the camera ray traced ahead or not
-    all give the same bits as one lane without the tail kernel."""
+    (off, every walk heavy, the default), the camera ray traced ahead or not and
+    the fast lane all give the same bits as one lane without the tail kernel."""
     import scenes
     from hip_mem import DeviceBuffer
     P = rt_amd.parse_obj(scenes.scene_path("dragon_small"))
     sky = scenes.make_sky("L")
     W, H, spp, nb = 640, 480, 2, 8
 
-    def render(lanes, tail, off=0, stride=1, heavy=6, enter=2.0, spec_cam=1, rows=1, drain=4, tail_cam=0):
+    def render(lanes, tail, off=0, stride=1, heavy=6, enter=2.0, spec_cam=1, rows=1, drain=4, tail_cam=0, fast_k=0,
+               fast_spp=2.25):
         rk = rt_amd.RenderKernel(W, H, spp, nb, rt_amd.Image(1, 1), P.triangles, P.materials,
                                  P.emissive_triangle_indices, P.material_indices, None, rt_amd.BVH(P.triangles),
                                  rt_amd.Image.from_rgb(sky), None, device=0)
         rk.test_schedule(lanes=lanes, tail_paths=tail, heavy_calls=heavy, tail_enter=enter, spec_cam=spec_cam,
-                         tail_rows=rows, drain_rows=drain, tail_spec_cam=tail_cam)
+                         tail_rows=rows, drain_rows=drain, tail_spec_cam=tail_cam, fast_k=fast_k, fast_spp=fast_spp)
         rk.set_camera(rt_amd.Camera.preset("dragon"))
         rows = len(range(off, H, stride))
         init = np.zeros((rows, W, 4), np.float32)
@@ -322,6 +323,14 @@ def test_gpu_schedules_bit_identical():
         got = render(3, tail, enter=enter, rows=rows, drain=drain)
         np.testing.assert_array_equal(got.view(np.uint32), base.view(np.uint32),
                                       err_msg=f"rows={rows} tail={tail} drain={drain}")
+    # the fast lane: the slowest paths of every lane handed to one tail kernel on a stream of its
+    # own (a few, or most of the paths; early or late; with 1, 3 and 4 lanes; with and without the
+    # lanes' own tail kernel), the rest still in the wavefront; and the product's default
+    for lanes, tail, fast_k, fast_spp in ((1, 1, 64, 0.0), (3, 1, 768, 2.25), (4, 1, 4096, 0.5), (3, 0, 256, 1.0),
+                                          (2, 2, 100000, 0.0), (0, -1, -1, -1.0)):
+        got = render(lanes, tail, fast_k=fast_k, fast_spp=fast_spp)
+        np.testing.assert_array_equal(got.view(np.uint32), base.view(np.uint32),
+                                      err_msg=f"fast_k={fast_k} fast_spp={fast_spp} lanes={lanes} tail={tail}")
 
 
 @pytest.mark.gpu
