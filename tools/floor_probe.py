@@ -30,7 +30,7 @@ def main():
                              P.emissive_triangle_indices, P.material_indices, None, rt_amd.BVH(P.triangles),
                              rt_amd.Image.from_rgb(sky), None, device=0)
     rk.set_camera(rt_amd.Camera(cam17[:16], cam17[16]))
-    rk.test_schedule(tail_paths=0, lanes=1)  # (no tail kernel: every iteration a k_trace + k_step pair)
+    rk.test_schedule(tail_paths=0, lanes=1, fast_k=0)  # (no tail kernel: every iteration a k_trace + k_step pair)
     dev = torch.device("cuda", 0)
     fr = ShardedFrame(rk, 0, 1, device=dev)
     stream = torch.cuda.current_stream(dev).cuda_stream

@@ -3,6 +3,8 @@
 
   python tools/rocpd_summary.py trace DB          -> kernel stats table
   python tools/rocpd_summary.py pmc DB [DB ...]   -> counters per kernel
+  python tools/rocpd_summary.py gaps DB [JSON]    -> per stream: the idle time between one
+                                                     kernel's end and the next one's start
 """
 import sqlite3
 import sys
@@ -60,7 +62,46 @@ def pmc(dbs, as_json=None):
             print(f"   {cn:32s} {v:18.4g}")
 
 
+def gaps(db, as_json=None):
+    """Per stream (queue when the trace has no stream id), consecutive dispatches: the gap
+    from one kernel's end to the next's start, split at 20 us (launch / dependency gaps vs
+    host round trips), and per kernel pair."""
+    import json
+    c = sqlite3.connect(db)
+    cols = [r[1] for r in c.execute("pragma table_info(kernels)")]
+    sid = [x for x in ("stream_id", "queue_id") if x in cols]
+    key = sid[0] if sid else None
+    rows = c.execute(f"select name, start, end{', ' + key if key else ''} from kernels order by start").fetchall()
+    by = defaultdict(list)
+    for r in rows:
+        by[r[3] if key else 0].append((short(r[0]), r[1], r[2]))
+    out = {"columns": cols, "group_by": key, "streams": {}}
+    for s_, ks in by.items():
+        g = [(ks[i - 1][0] + "->" + ks[i][0], (ks[i][1] - ks[i - 1][2]) / 1e3) for i in range(1, len(ks))]
+        short_g = [x for _, x in g if x < 20.0]
+        pairs = defaultdict(list)
+        for pn, x in g:
+            if x < 20.0:
+                pairs[pn].append(x)
+        srt = sorted(short_g)
+        out["streams"][str(s_)] = {
+            "kernels": len(ks), "gaps_under_20us": len(short_g),
+            "median_us": round(srt[len(srt) // 2], 2) if srt else None,
+            "mean_us": round(sum(srt) / len(srt), 2) if srt else None,
+            "gaps_over_20us": sum(1 for _, x in g if x >= 20.0),
+            "over_20us_total_ms": round(sum(x for _, x in g if x >= 20.0) / 1e3, 3),
+            "pairs": {k: {"n": len(v), "median_us": round(sorted(v)[len(v) // 2], 2)} for k, v in pairs.items() if len(v) >= 4}}
+    txt = json.dumps(out, indent=1)
+    print(txt)
+    if as_json:
+        with open(as_json, "w") as f:
+            f.write(txt)
+
+
 if __name__ == "__main__":
+    if sys.argv[1] == "gaps":
+        gaps(sys.argv[2], sys.argv[3] if len(sys.argv) > 3 else None)
+        sys.exit(0)
     if sys.argv[1] == "trace":
         trace(sys.argv[2])
     elif sys.argv[1] == "pmcjson":
