@@ -88,11 +88,11 @@ CFG5_ROUGH = [0.05, 0.25, 0.5, 1.0]
 CFG5_ORDER = [0, 4, 8, 12, 1, 5, 9, 13, 3, 7, 11, 15, 2, 6, 10, 14]
 HBM_PEAK_GBS = 8000.0  # /opt/skills/guides/MI355X_MICROARCH.md (spec)
 # Algorithmic bytes per unit of work: the records a query
-# must read. Search-BVH box test 32 B (one child record), triangle test
+# must read. Search-BVH box test 48 B (one child record + its oriented slab, r05), triangle test
 # 48 B (a, e1, e2 as 3 x 16 B), octree verification slab test 64 B (one
 # record), queue ray 32 B + result 8 B per query; step kernel: material
 # 32 B, env texel 16 B, env-CDF fence load 64 B (16 keys; rt_trace.h fence_count).
-BYTES = {"box": 32, "tri": 48, "verify": 64, "ray": 40, "mat": 32, "env": 16, "cdf": 64}
+BYTES = {"box": 48, "tri": 48, "verify": 64, "ray": 40, "mat": 32, "env": 16, "cdf": 64}
 # the reference's octree walk, 56 B per child-volume test, 36 B per triangle
 REF_BYTES = {"vol": 56, "tri": 36}
 
@@ -664,8 +664,8 @@ def main():
                     "occlusion_box_tests": None if stats_seq is None else
                     {"executed": stats["any_vol"] - stats.get("tail_any_vol", 0),
                      "necessary": stats_seq["any_vol"] - stats_seq.get("tail_any_vol", 0)},
-                    "byte_model": "records a query must read (bench.py BYTES): 32 B per search-BVH box test (one "
-                                  "child record), 48 B per triangle test, 64 B per octree verification slab test, "
+                    "byte_model": "records a query must read (bench.py BYTES): 48 B per search-BVH box test (one "
+                                  "child record + its 16-B oriented slab), 48 B per triangle test, 64 B per octree verification slab test, "
                                   "40 B per query (queue ray + result); box tests counted as executed, incl. the "
                                   "paired occlusion trips' stack-top node",
                     "traffic": load_traffic(tkey) if (n_gpus == 1 and not args.sim_world) else None,
