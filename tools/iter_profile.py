@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--config", default="cfg2")
     ap.add_argument("--world", type=int, default=1)
     ap.add_argument("--lanes", type=int, default=1)
+    ap.add_argument("--fast-k", type=int, default=0, help="fast lane paths (0 off: r04-comparable bands; -1 product)")
     ap.add_argument("--out", default="gpurun_out/iter")
     ap.add_argument("--raw", action="store_true", help="add the per-iteration arrays")
     args = ap.parse_args()
@@ -41,6 +42,7 @@ def main():
                              rt_amd.Image.from_rgb(sky), None, device=0)
     rk.set_camera(rt_amd.Camera(cam17[:16], cam17[16]))
     rk.set_lanes(args.lanes)
+    rk.test_schedule(fast_k=args.fast_k)
     dev = torch.device("cuda", 0)
     fr = ShardedFrame(rk, 0, args.world, device=dev)
     stream = torch.cuda.current_stream(dev).cuda_stream
