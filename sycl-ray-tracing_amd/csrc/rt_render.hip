@@ -173,6 +173,7 @@ struct Backend {
     rtk::WaveView* h_fviews = nullptr;  // pinned
     hipEvent_t fev[RT_MAX_LANES] = {}, fev_done = nullptr;
     bool fev_done_recorded = false;
+    hipEvent_t ftev[2] = {};  // (timed renders: around the fast lane's kernel)
     hipStream_t fs = nullptr;  // the fast lane's stream with 4 lanes (fewer: the first idle lane stream)
     DevBuf xy;        // pixel list (rt_render_pixels)
     DevBuf fb;        // host-fb staging
@@ -1606,6 +1607,8 @@ void destroy_one(Backend* b)
     if (b->h_fviews) (void)hipHostFree(b->h_fviews);
     if (b->fev_done) (void)hipEventDestroy(b->fev_done);
     if (b->fs) (void)hipStreamDestroy(b->fs);
+    for (hipEvent_t e : b->ftev)
+        if (e) (void)hipEventDestroy(e);
     for (int l = 0; l < RT_MAX_LANES; l++) {
         if (b->h_act[l]) (void)hipHostFree(b->h_act[l]);
         if (b->ev_lane[l]) (void)hipEventDestroy(b->ev_lane[l]);
@@ -2042,6 +2045,11 @@ int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounces, cons
         HIPCHK(c, hipMemcpyAsync(b->fviews.p, b->h_fviews, sizeof(rtk::WaveView) * RT_MAX_LANES, hipMemcpyHostToDevice,
                                  fstream));
         const rtk::WaveView* fv = (const rtk::WaveView*)b->fviews.p;
+        if (b->timing) {
+            for (hipEvent_t& e : b->ftev)
+                if (!e) HIPCHK(c, hipEventCreate(&e));
+            HIPCHK(c, hipEventRecord(b->ftev[0], fstream));
+        }
         const int4 parts = make_int4(start[0], start[1], start[2], start[3]);
         if (SEQ)
             hipLaunchKernelGGL((k_tail_fast<true, false, 4>), dim3(tot), dim3(threads), 0, fstream, fv, parts, stats);
@@ -2050,6 +2058,7 @@ int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounces, cons
         else
             hipLaunchKernelGGL((k_tail_fast<false, true, 16>), dim3(tot), dim3(threads), 0, fstream, fv, parts, stats);
         HIPCHK(c, hipGetLastError());
+        if (b->timing) HIPCHK(c, hipEventRecord(b->ftev[1], fstream));
         HIPCHK(c, hipEventRecord(b->fev_done, fstream));
         b->fev_done_recorded = fast_ran = true;
         return RT_OK;
@@ -2269,7 +2278,8 @@ int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounces, cons
         if (lf) fclose(lf);
         // RT_TIMELINE=file: every lane's launches on one clock (ms from lane 0's first
         // k_trace): lane, iteration, k_trace start, k_trace end = k_step start, k_step end,
-        // 1 for the tail kernel (tools/timeline.py)
+        // 1 for the tail kernel (tools/timeline.py); the fast lane's kernel as lane `lanes`,
+        // iteration 0, flag 2
         // (device index d > 0 of a multi-device context writes file.d: the device threads run concurrently)
         if (!dg.timeline.empty()) {
             const char* tl = dg.timeline.c_str();
@@ -2283,6 +2293,12 @@ int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounces, cons
                              i == L[l].tail_iter ? 1 : 0);
                     rows += line;
                 }
+            if (fast_ran) {
+                float t[2];
+                for (int k = 0; k < 2; k++) HIPCHK(c, hipEventElapsedTime(&t[k], L[0].tev[0][0], b->ftev[k]));
+                snprintf(line, sizeof line, "%d 0 %.4f %.4f %.4f 2\n", nl, t[0], t[1], t[1]);
+                rows += line;
+            }
             const std::string path = b->index > 0 ? std::string(tl) + "." + std::to_string(b->index) : std::string(tl);
             if (FILE* f = fopen(path.c_str(), "w")) {
                 fwrite(rows.data(), 1, rows.size(), f);

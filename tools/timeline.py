@@ -25,9 +25,14 @@ for p in (os.path.join(REPO, "sycl-ray-tracing_amd"), os.path.join(REPO, "tools"
 
 
 def summarize(rows: np.ndarray) -> dict:
-    """rows: lane, iter, trace start, trace end, step end, tail flag (ms)."""
+    """rows: lane, iter, trace start, trace end, step end, flag (1 tail kernel, 2 the fast lane's kernel) (ms)."""
+    fast = rows[rows[:, 5] == 2]  # (the fast lane's kernel: start, end)
+    rows = rows[rows[:, 5] != 2]
     lanes = sorted(set(int(x) for x in rows[:, 0]))
     out = {"lanes": []}
+    if len(fast):
+        out["fast_lane"] = {"start_ms": round(float(fast[0, 2]), 2), "end_ms": round(float(fast[0, 3]), 2),
+                            "ms": round(float(fast[0, 3] - fast[0, 2]), 2)}
     ev = []  # (time, +1 / -1) per lane busy interval (first launch .. last)
     for l in lanes:
         r = rows[rows[:, 0] == l]
@@ -49,7 +54,7 @@ def summarize(rows: np.ndarray) -> dict:
         busy[cur] = busy.get(cur, 0.0) + (t - last)
         cur += dlt
         last = t
-    out["frame_ms"] = round(float(rows[:, 4].max() - rows[:, 2].min()), 3)
+    out["frame_ms"] = round(float(max(rows[:, 4].max(), fast[:, 3].max() if len(fast) else 0.0) - rows[:, 2].min()), 3)
     out["ms_with_n_lanes_busy"] = {str(k): round(v, 2) for k, v in sorted(busy.items())}
     return out
 
