@@ -15,9 +15,9 @@ def short(name):
     import re
     m = re.search(r"k_[a-z_]+(?:<[^>]*>)?", name)
     n = m.group(0) if m else name[:60]
-    t = re.search(r"ILb(\d)E(?:Lb(\d)E)?", name)
+    t = re.search(r"I((?:L[bi]\d+E)+)", name)
     if t:
-        n += "<" + ",".join(x for x in t.groups() if x is not None) + ">"
+        n += "<" + ",".join(re.findall(r"L[bi](\d+)E", t.group(1))) + ">"
     return n
 
 
