@@ -445,8 +445,10 @@ __global__ __launch_bounds__(256) void k_tonemap(rtk::WaveView W)
 #define RT_REFILL 16
 #define RT_QSTACK 32            // quad walks (rt_quad.h): stack entries per quad (item + key, 64 quads per block)
 #define RT_RSTACK 64            // row walks (rt_row.h): stack entries per row (item + key, 16 rows per block)
+#ifndef RT_TRACE_REFILL
 #define RT_TRACE_REFILL 4       // k_trace: idle quads of a wave that trigger a refill from its query stream
                                 // (r02, cfg2: 4 / 8 -> 726 / 723 vs 678 Msamples/s with static 16-query chunks)
+#endif
 #ifndef RT_HEAVY_CALLS
 #define RT_HEAVY_CALLS 6        // heavy class (seg_id): quad_visit calls of a walk that flag its path (0: off).
                                 // cfg2 (r02): off / 3 / 6 / 10 / 16 -> 737 / 744 / 744-748 / 740 / 735 Msamples/s;
