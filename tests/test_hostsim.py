@@ -64,6 +64,23 @@ def test_schedule_is_not_read_from_the_environment(manifest, cameras, monkeypatc
         rk.test_schedule(no_such_knob=1)
 
 
+def test_schedule_keys(manifest, cameras):
+    """Every rt_test_schedule key the tests and tools use (include/rt_hip.h) is
+    accepted, `reset` restores the product schedule, and the frame is the same either way (the
+    hostsim backend ignores the GPU-only keys: lanes, tail kernel, fast lane)."""
+    e = rt_cases.golden_case(rt_cases.CORNELL_CASES[0], manifest)
+    rk, fb = rt_cases.make_kernel(e, cameras, hostsim=True)
+    rk.test_schedule(lanes=2, tail_paths=1, tail_enter=1.5, tail_rows=0, drain_rows=1, heavy_calls=0, spec_cam=2,
+                     tail_spec_cam=1, force_fallback=0, step_budget=64, fast_k=512, fast_spp=1.0)
+    rk.render()
+    assert gio.compare_rgb(fb.pixels, e["expected"])["bitwise_fraction"] == 1.0
+    rk2, fb2 = rt_cases.make_kernel(e, cameras, hostsim=True)  # (a render writes over a fresh frame)
+    rk2.test_schedule(fast_k=7)
+    rk2.test_schedule(reset=1)
+    rk2.render()
+    assert gio.compare_rgb(fb2.pixels, e["expected"])["bitwise_fraction"] == 1.0
+
+
 @pytest.mark.slow
 @pytest.mark.parametrize("name", ["cfg2_dragon", "cfg4_dragon4k", "cfg5_sweep_m0_r0", "cfg5_sweep_m3_r3"])
 def test_hostsim_dragon_bit_exact(name, manifest, cameras):
