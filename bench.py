@@ -670,6 +670,11 @@ def main():
                                   "paired occlusion trips' stack-top node",
                     "traffic": load_traffic(tkey) if (n_gpus == 1 and not args.sim_world) else None,
                     "traffic_source": traffic_source(tkey) if (n_gpus == 1 and not args.sim_world) else None,
+                    # (the measured fabric bytes per launch / the launch's time / peak: what HBM actually
+                    # moved, vs frac's algorithmic bytes; most records are served by L2 and the MALL)
+                    "traffic_frac": (round(load_traffic(tkey) / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+                                     if (n_gpus == 1 and not args.sim_world and load_traffic(tkey) and avg_ms > 0)
+                                     else None),
                     "measured": "1-lane render after the timed steps (one stream: launches do not overlap); "
                                 "HIP events around each launch",
                     "algo_bytes_per_launch": round(algo), "avg_launch_ms": round(avg_ms, 4),
