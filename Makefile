@@ -29,11 +29,15 @@ $(OBJ)/%.host.o: $(SRC)/%.cpp $(HDRS)
 	@mkdir -p $(OBJ)
 	$(CXX) $(CXXFLAGS) -c $< -o $@
 
-$(OBJ)/rt_hostsim.o: $(SRC)/rt_hostsim.cpp $(HDRS)
+# (the two objects that compile SRC_HASH in as rt_build_id depend on every file it hashes,
+# so a change to a host-only source cannot leave a stale build id in the library)
+ALL_SRC := $(wildcard $(SRC)/*) $(wildcard include/*.h)
+
+$(OBJ)/rt_hostsim.o: $(SRC)/rt_hostsim.cpp $(HDRS) $(ALL_SRC)
 	@mkdir -p $(OBJ)
 	$(CXX) $(CXXFLAGS) -fopenmp -DRT_BUILD_SRC='"$(SRC_HASH)"' -c $< -o $@
 
-$(OBJ)/rt_render.o: $(SRC)/rt_render.hip $(HDRS)
+$(OBJ)/rt_render.o: $(SRC)/rt_render.hip $(HDRS) $(ALL_SRC)
 	@mkdir -p $(OBJ)
 	$(HIPCC) $(HIPFLAGS) -DRT_BUILD_SRC='"$(SRC_HASH)"' -c $< -o $@
 
@@ -82,6 +86,15 @@ variant: $(OBJ)/rt_scene.host.o $(OBJ)/rt_imageio.host.o $(OBJ)/rt_capi_host.hos
 	@mkdir -p $(LIB)
 	$(HIPCC) $(HIPFLAGS) $(DEFS) -DRT_BUILD_SRC='"$(SRC_HASH)"' -DRT_BUILD_DEFS='"$(DEFS)"' -c $(SRC)/rt_render.hip -o $(OBJ)/rt_render_$(V).o
 	$(HIPCC) -shared --offload-arch=$(ARCH) -fPIC $(OBJ)/rt_render_$(V).o $^ -o $(LIB)/librt_hip_$(V).so
+
+# the same for the hostsim build: make hostsim-variant V=name DEFS="-DRT_SLABS=0" ->
+# lib/librt_hostsim_name.so (RT_HOSTSIM_LIB=...; study probes such as tools/far_probe.py)
+hostsim-variant: $(OBJ)/rt_imageio.host.o
+	@mkdir -p $(LIB)
+	$(CXX) $(CXXFLAGS) -fopenmp $(DEFS) -DRT_BUILD_SRC='"$(SRC_HASH)"' -DRT_BUILD_DEFS='"$(DEFS)"' -c $(SRC)/rt_hostsim.cpp -o $(OBJ)/rt_hostsim_$(V).o
+	$(CXX) $(CXXFLAGS) $(DEFS) -c $(SRC)/rt_scene.cpp -o $(OBJ)/rt_scene_$(V).o
+	$(CXX) $(CXXFLAGS) $(DEFS) -c $(SRC)/rt_capi_host.cpp -o $(OBJ)/rt_capi_host_$(V).o
+	$(CXX) -shared -fopenmp $(OBJ)/rt_hostsim_$(V).o $(OBJ)/rt_scene_$(V).o $(OBJ)/rt_capi_host_$(V).o $(OBJ)/rt_imageio.host.o -o $(LIB)/librt_hostsim_$(V).so
 
 # C++ drop-in check (container only): include/render_kernel_hip.h against the
 # reference's headers and objects (oracle/_ref, `make ref`), linked to the hostsim

@@ -632,6 +632,9 @@ def main():
     ktime, lane1_ms = None, None
     if not args.no_roofline_pass or args.roofline_only:
         rk.set_lanes(1)
+        # (no fast lane either: its tail kernel would run on a second stream beside the
+        # k_trace launches being timed; the pass is one stream, launches never overlap)
+        rk.test_schedule(fast_k=0)
         frame.render(stream)  # (warm: the 1-lane wave buffers)
         torch.cuda.synchronize(dev)
         rk.kernel_timing(1)
@@ -641,6 +644,7 @@ def main():
         lane1_ms = (time.perf_counter() - t1) * 1e3
         ktime = rk.kernel_timing(0)
         rk.set_lanes(0)  # (auto)
+        rk.test_schedule(reset=1)  # (the product's schedule again)
         log(f"[rank {rank}] 1-lane render {lane1_ms:.1f} ms, kernel time per class {ktime}")
 
     samples_rank = frame.rows * W * spp if not single_process_multi else W * H * spp
@@ -654,6 +658,9 @@ def main():
         if stats_seq is not None:
             necessary = algo_bytes(stats_seq, "trace") / max(launches, 1) / (avg_ms * 1e-3) / 1e9
         tkey = f"{args.config}_1lane"
+        tsrc = traffic_source(tkey) if (n_gpus == 1 and not args.sim_world) else None
+        # (the committed PMC bytes count only if they were taken on the running build)
+        traffic = load_traffic(tkey) if (tsrc and tsrc["same_build"]) else None
         roofline = {"bound": "hbm", "kernel": "k_trace", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                     "achieved_necessary": None if necessary is None else round(necessary, 1),
@@ -668,15 +675,15 @@ def main():
                                   "child record + its 16-B oriented slab), 48 B per triangle test, 64 B per octree verification slab test, "
                                   "40 B per query (queue ray + result); box tests counted as executed, incl. the "
                                   "paired occlusion trips' stack-top node",
-                    "traffic": load_traffic(tkey) if (n_gpus == 1 and not args.sim_world) else None,
-                    "traffic_source": traffic_source(tkey) if (n_gpus == 1 and not args.sim_world) else None,
+                    "traffic": traffic,
+                    "traffic_source": tsrc,
                     # (the measured fabric bytes per launch / the launch's time / peak: what HBM actually
-                    # moved, vs frac's algorithmic bytes; most records are served by L2 and the MALL)
-                    "traffic_frac": (round(load_traffic(tkey) / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
-                                     if (n_gpus == 1 and not args.sim_world and load_traffic(tkey) and avg_ms > 0)
-                                     else None),
-                    "measured": "1-lane render after the timed steps (one stream: launches do not overlap); "
-                                "HIP events around each launch",
+                    # moved, vs frac's algorithmic bytes; most records are served by L2 and the MALL;
+                    # null when the committed profile is of another build)
+                    "traffic_frac": (round(traffic / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+                                     if (traffic and avg_ms > 0) else None),
+                    "measured": "1-lane render after the timed steps, fast lane off (one stream: launches do "
+                                "not overlap); HIP events around each launch",
                     "algo_bytes_per_launch": round(algo), "avg_launch_ms": round(avg_ms, 4),
                     "launches_per_render": launches,
                     "kernel_ms_per_render_1lane": {k: round(v[0], 2) for k, v in ktime.items()},
@@ -688,7 +695,7 @@ def main():
         # fences) and with the wavefront's slot records; traffic = committed FETCH_SIZE pass
         sm = step_model_bytes(stats, samples_rank)
         s_launches = ktime["step"][1]
-        tr = load_traffic_class(f"{args.config}_1lane", "k_step") if (n_gpus == 1 and not args.sim_world) else None
+        tr = load_traffic_class(f"{args.config}_1lane", "k_step") if (tsrc and tsrc["same_build"]) else None
         roofline["k_step"] = {
             "model_scene_bytes_per_launch": round(sm["scene"] / max(s_launches, 1)),
             "model_with_slots_bytes_per_launch": round((sm["scene"] + sm["slot"]) / max(s_launches, 1)),
@@ -768,6 +775,13 @@ def main():
         }
         if strong is not None:
             out["strong_cfg4"] = strong
+            # the north star's fixed-size figure beside the weak-scaling value: cfg4 (its 8-GPU
+            # config) split over these N GPUs against the same frame on one, T_1 / (N T_N)
+            out["scaling_fixed_size"] = {"config": "cfg4", "kind": "strong", "n_gpus": n_gpus,
+                                         "efficiency": strong["efficiency"], "ms_1gpu": strong["ms_1gpu"],
+                                         "ms_n_gpus": strong["ms_n_gpus"],
+                                         "note": f"`value` is {args.scaling} scaling ({args.config}); this is "
+                                                 f"cfg4's fixed-size split over the same {n_gpus} GPUs"}
         print(json.dumps(out), flush=True)
     # a frame that differs from the reference's (N = 1: the CPU port's rows, 1e-4 per channel
     # after tone-map; N > 1: the gathered frame against one device's, bitwise) fails the run

@@ -67,14 +67,23 @@ int rt_device_count(const rt_context* ctx);
  * fails device d (0..n-1) before its work starts (-1: off), to exercise the
  * per-device error slots. Never called by the product paths. */
 int rt_create_multi_loopback(int n_devices, const int* devices, rt_context** out);
+/* TEST ONLY. rt_test_create_multi_rccl: as rt_create_multi, but the multi-device
+ * driver runs even for one listed device, through a one-rank RCCL clique
+ * (ncclCommInitAll over [device]): pack, ncclScatter, render, ncclGather and
+ * un-permute, so that a one-GPU box executes the RCCL path the 8-GPU node runs. */
+int rt_test_create_multi_rccl(int n_devices, const int* devices, rt_context** out);
 int rt_test_fail_device(rt_context* ctx, int device);
 /* TEST ONLY. rt_test_schedule: override one wavefront-schedule parameter of
  * ctx's later renders (keys: "lanes", "tail_paths" (0: no tail kernel),
  * "tail_enter", "tail_rows", "drain_rows", "heavy_calls", "spec_cam",
- * "tail_spec_cam", "step_budget", the stressor "force_fallback" (every k-th
- * query by a ray hash skips to the exact octree walk), "reset"). No parameter
- * changes a result; the product never calls it and reads no schedule from the
- * environment. RT_ERR_ARG for an unknown key. */
+ * "tail_spec_cam", "step_budget", "fast_k" (fast lane: that many of the slowest
+ * paths go to a tail kernel early; 0: off), "fast_spp" (... from iteration
+ * fast_spp x spp on), "near_scale" (the near box, scene box widened by this x its
+ * largest extent: queries from outside it take the exact octree walk), the
+ * stressor "force_fallback" (every k-th query by a ray hash skips to the exact
+ * octree walk), "reset"). No parameter changes a result; the product never calls
+ * it and reads no schedule from the environment. RT_ERR_ARG for an unknown key or
+ * a value that is not a finite number in int range. */
 int rt_test_schedule(rt_context* ctx, const char* key, double value);
 /* TEST ONLY. Walk log of stats renders (rt_set_stats): every search-BVH walk of
  * at least min_calls quad_visit calls (a row trip counts 2) is recorded, up to

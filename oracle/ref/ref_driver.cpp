@@ -85,6 +85,11 @@ static Camera camera_by_name(const std::string& n)  // camera.cpp:3-8
     if (n == "dragon") return Camera::PBRT_DRAGON_CAMERA;
     if (n == "mis") return Camera::MIS_CAMERA;
     if (n == "default") return Camera();
+    // "tele:fov:rx:tx:ty:tz": a camera built the way camera.cpp:3-8 builds the presets,
+    // Camera(fov, RotationX(rx) * Translation(tx, ty, tz)) (far telephoto fixtures)
+    float fov, rx, tx, ty, tz;
+    if (std::sscanf(n.c_str(), "tele:%f:%f:%f:%f:%f", &fov, &rx, &tx, &ty, &tz) == 5)
+        return Camera(fov, RotationX(rx) * Translation(tx, ty, tz));
     std::fprintf(stderr, "unknown camera %s\n", n.c_str());
     std::exit(1);
 }

@@ -2,6 +2,7 @@
 // (include/rt_hip.h): argument checking, host scene preparation, host
 // helpers. The compute half lives in rt_render.hip (gfx950).
 #include <algorithm>
+#include <cmath>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
@@ -76,7 +77,34 @@ RtSceneView rt_host_view(const rt_context* c)
     v.parent = c->flat.parent.data();
     v.leaf_of = c->flat.leaf_of.data();
     v.tri_mat = 0;
+    rt_view_near(c, v);
     return v;
+}
+
+void rt_view_near(const rt_context* c, RtSceneView& v)
+{
+    const double scale = c->sched.near_scale >= 0.0 ? c->sched.near_scale : RT_NEAR_SCALE;
+    // the scene's box: the octree root's axis planes (PLANE_NORMALS 0-2 are the axes: the
+    // vertices' min / max) and every analytic sphere's box
+    double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY}, ext = 0.0;
+    if (!c->flat.nodes.empty())
+        for (int i = 0; i < 3; i++) lo[i] = c->flat.nodes[0].dn[i], hi[i] = c->flat.nodes[0].df[i];
+    for (size_t k = 0; k + 1 < c->spheres.size(); k += 2) {
+        const float4_& sp = c->spheres[k];
+        const double cc[3] = {sp.x, sp.y, sp.z}, r = std::fabs((double)sp.w);
+        for (int i = 0; i < 3; i++) lo[i] = std::min(lo[i], cc[i] - r), hi[i] = std::max(hi[i], cc[i] + r);
+    }
+    bool have = true;
+    for (int i = 0; i < 3; i++) {
+        if (!(lo[i] <= hi[i]) || !std::isfinite(lo[i]) || !std::isfinite(hi[i])) have = false;
+        else ext = std::max(ext, hi[i] - lo[i]);
+    }
+    for (int i = 0; i < 3; i++) {
+        const double w = have ? scale * ext : 0.0;
+        // rounded outwards; beyond float range (or no scene): unbounded
+        v.near_lo[i] = have ? std::nextafter((float)(lo[i] - w), -INFINITY) : -INFINITY;
+        v.near_hi[i] = have ? std::nextafter((float)(hi[i] + w), INFINITY) : INFINITY;
+    }
 }
 
 bool rt_table_has_emissive_prim(const rt_context* c, const RtMat* table)
@@ -128,7 +156,10 @@ namespace {
 // checked against the devices present when the backend opens them (RT_ERR_NODEV).
 // loopback (rt_create_multi_loopback, tests only) admits a list that names a GPU more
 // than once: the context then exchanges the shards with device copies instead of RCCL.
-int create_multi(int n_devices, const int* devices, bool loopback, rt_context** out)
+// rccl (rt_test_create_multi_rccl, tests only): the multi-device driver and its RCCL clique
+// even for one listed device (a one-rank ncclCommInitAll), so a one-GPU box runs the pack,
+// ncclScatter, render, ncclGather and un-permute sequence the 8-GPU node runs.
+int create_multi(int n_devices, const int* devices, bool loopback, rt_context** out, bool rccl = false)
 {
     if (!out) return rt_fail(nullptr, RT_ERR_ARG, "rt_create_multi: out is NULL");
     *out = nullptr;
@@ -144,6 +175,7 @@ int create_multi(int n_devices, const int* devices, bool loopback, rt_context** 
     for (int d = 0; d < n_devices; d++) c->devices.push_back(devices ? devices[d] : d);
     c->device = c->devices[0];
     c->loopback = loopback;
+    c->force_multi = rccl;
     rt_read_diag(c);
     int r = rt_backend_create(c);
     if (r) {
@@ -168,6 +200,11 @@ int rt_create_multi_loopback(int n_devices, const int* devices, rt_context** out
     return create_multi(n_devices, devices, true, out);
 }
 
+int rt_test_create_multi_rccl(int n_devices, const int* devices, rt_context** out)
+{
+    return create_multi(n_devices, devices, false, out, true);
+}
+
 int rt_test_fail_device(rt_context* c, int device)
 {
     if (!c) return rt_fail(nullptr, RT_ERR_ARG, "rt_test_fail_device: ctx is NULL");
@@ -180,7 +217,11 @@ int rt_test_schedule(rt_context* c, const char* key, double value)
     if (!c || !key) return rt_fail(c, RT_ERR_ARG, "rt_test_schedule: ctx or key is NULL");
     RtSchedule& s = c->sched;
     const std::string k = key;
-    const int v = (int)value;
+    // (finite for every key; in int range for the integer ones: the cast is otherwise undefined)
+    const bool real_key = k == "tail_enter" || k == "fast_spp" || k == "near_scale";
+    if (!std::isfinite(value) || (!real_key && (value < -2147483648.0 || value > 2147483647.0)))
+        return rt_fail(c, RT_ERR_ARG, "rt_test_schedule: value of " + k + " is out of range");
+    const int v = real_key ? 0 : (int)value;
     if (k == "lanes") s.lanes = std::max(0, v);
     else if (k == "tail_paths") s.tail_paths = v;
     else if (k == "tail_enter") s.tail_enter = value;
@@ -193,6 +234,7 @@ int rt_test_schedule(rt_context* c, const char* key, double value)
     else if (k == "step_budget") s.step_budget = v;
     else if (k == "fast_k") s.fast_k = v;
     else if (k == "fast_spp") s.fast_spp = value;
+    else if (k == "near_scale") s.near_scale = value;
     else if (k == "reset") s = RtSchedule{};
     else return rt_fail(c, RT_ERR_ARG, "rt_test_schedule: unknown key " + k);
     return RT_OK;

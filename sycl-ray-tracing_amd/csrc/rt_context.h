@@ -32,6 +32,8 @@ struct RtSchedule {
     int step_budget = -1;      // exact-walk steps per query per launch before it parks
     int fast_k = -1;           // fast lane: this many of the slowest paths to a tail kernel early (0: off)
     double fast_spp = -1.0;    // ... at the lanes' first readback from iteration fast_spp x spp on
+    double near_scale = -1.0;  // near box: the scene's box widened by this x its largest extent (rt_view_near;
+                               // study probes only: answers never depend on it, only which walk gives them)
 };
 
 // Diagnostics, read from the environment once when the context is created (rt_create*):
@@ -56,6 +58,7 @@ struct rt_context {
     // One entry: a single-device context on that ordinal (nothing to shard, no RCCL)
     std::vector<int> devices;
     bool loopback = false;        // devices may repeat: shards exchanged by device copies, not RCCL
+    bool force_multi = false;     // (rt_test_create_multi_rccl) the multi-device driver and RCCL even for one device
     int fail_device = -1;         // rt_test_fail_device (tests only): that device fails its share
     std::string err;
 
@@ -142,6 +145,13 @@ int rt_for_devices(rt_context* c, int n, F fn)
     return 0;
 }
 RtSceneView rt_host_view(const rt_context* ctx);  // host-memory view (hostsim)
+// The view's near box (rt_fast.h far_origin): the octree root's axis planes (the scene's box)
+// widened on every side by RT_NEAR_SCALE (or sched.near_scale) x the box's largest extent;
+// unbounded for an empty scene.
+#ifndef RT_NEAR_SCALE
+#define RT_NEAR_SCALE 1.0
+#endif
+void rt_view_near(const rt_context* ctx, RtSceneView& v);
 // Does any primitive (triangle or sphere) use a material with a positive
 // emission component (the test at render_kernel.cpp:696)? If not, the
 // BRDF->light query of sample_light_sources can never contribute.

@@ -110,6 +110,9 @@ struct RtSceneView {
     const int32_t* parent;     // octree record -> parent record (-1 for the root)
     const int32_t* leaf_of;    // leaf-order triangle k -> its octree leaf record
     int32_t tri_mat;  // 1: tri4[3k + 1].w holds the material index of leaf-order triangle k (device copy)
+    // near box (rt_fast.h far_origin): a query whose origin lies outside it is answered by the exact
+    // octree walk; the scene's box widened by RT_NEAR_SCALE x its largest extent (rt_view_near)
+    float near_lo[3], near_hi[3];
 };
 
 struct RtCamera {

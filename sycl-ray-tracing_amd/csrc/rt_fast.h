@@ -551,11 +551,66 @@ RT_HD int fast_any_u(const RtSceneView& S, V3 o, V3 d, STK& stk, Stats* st)
     }
 }
 
+// ---------------------------------------------------------------------------
+// Where the search BVH's answer cannot be trusted ("Far origins and grazing
+// hits"). Moller-Trumbore (triangle.h:24-44) computes s = o - a and then u = f (s.h),
+// v = f (d.q), t = f (e2.q): the rounding of the dot products is ~eps |s| |d| |e| while
+// det = e1.(d x e2) = |d| |e1 x e2| cos(theta) can be as small as 1e-7 (its only guard). The
+// u + v <= 1 and u <= 1 tests (and t) then carry an error of ~eps |s| / (sin(alpha) cos(theta)) in
+// space: the reference accepts rays that pass outside the triangle by that much. The search
+// BVH's boxes are padded by 1e-4 of their coordinates' magnitude (rt_scene.cpp pad_box), which
+// covers it only while |s| and the grazing factor stay moderate. Two cases go to the exact walk:
+//  * far_origin: the ray starts outside the near box (the scene's box widened by RT_NEAR_SCALE x
+//    its largest extent): |s| is unbounded there (profiles/r06_far_probe.json);
+//  * fuzzy_hit (RT_FUZZ_CHECK builds; off in the product): the found hit's own Moller-Trumbore
+//    fuzz eps |s| |d| |e1| |e2| / |det| exceeds RT_FUZZ_TAU x its box pad. A neighbour the walk
+//    did not enter (its fuzz beyond its pad) is usually a grazing triangle of the same surface,
+//    and the found hit then shares that conditioning. Measured (profiles/r06_far_origin.json):
+//    it removes most of the near grazing misses of the probe but costs cfg2 4 % at tau 1 (2 %
+//    the leaf-test arithmetic, 1.5 % the extra exact walks of grazing rays), so it stays off.
+#ifndef RT_FUZZ_CHECK
+#define RT_FUZZ_CHECK 0
+#endif
+#ifndef RT_FUZZ_TAU
+#define RT_FUZZ_TAU 1.0f
+#endif
+RT_HD bool far_origin(const RtSceneView& S, V3 o)
+{
+    return o.x < S.near_lo[0] || o.x > S.near_hi[0] || o.y < S.near_lo[1] || o.y > S.near_hi[1] ||
+           o.z < S.near_lo[2] || o.z > S.near_hi[2];
+}
+// Is the Moller-Trumbore answer for leaf-order triangle k (records a, e1, e2) fuzzier than
+// RT_FUZZ_TAU x the pad of its box? (squares: no division, no square root)
+RT_HD bool fuzzy_tri(float4_ ra, float4_ r1, float4_ r2, V3 o, V3 d)
+{
+    const V3 a = ld3(ra), e1 = ld3(r1), e2 = ld3(r2);
+    const float det = dot(e1, cross(d, e2));
+    const V3 s = sub(o, a);
+    auto amax = [](V3 v) { return __builtin_fmaxf(__builtin_fabsf(v.x), __builtin_fmaxf(__builtin_fabsf(v.y), __builtin_fabsf(v.z))); };
+#ifdef RT_FUZZ_LITE
+    const float m = __builtin_fmaxf(1.0f, amax(a));  // (<= the box's magnitude: flags a little more)
+#else
+    const float m = __builtin_fmaxf(__builtin_fmaxf(1.0f, amax(a)), __builtin_fmaxf(amax(add(a, e1)), amax(add(a, e2))));
+#endif
+    constexpr float c = 5.9604645e-8f / (1e-4f * RT_FUZZ_TAU);  // eps / (pad per unit magnitude x tau)
+    const float lhs = (c * c) * dot(s, s) * dot(d, d) * dot(e1, e1) * dot(e2, e2);
+    return !(lhs <= (m * m) * (det * det));  // (a NaN goes to the exact walk too)
+}
+// (device walks: quad_tri marks a fuzzy hit's octree leaf record with this bit; records < 2^30)
+#define RT_FZ_BIT 0x40000000
+RT_HD bool fuzzy_hit(const RtSceneView& S, int k, V3 o, V3 d)
+{
+    const float4_* r = S.tri4 + 3 * (size_t)k;
+    return fuzzy_tri(r[0], r[1], r[2], o, d);
+}
+
+
 // Closest-hit query answered through the BVH and verified against the
 // octree. Returns false when the answer must come from the exact walk.
 template <class STK, int WALK = RT_FAST_WALK_C>
 RT_HD bool fast_query_closest(const RtSceneView& S, V3 o, V3 d, STK& stk, float& t_out, int& k_out, Stats* st)
 {
+    if (far_origin(S, o)) return false;
     FastHit h;
     if (WALK == 1)
         fast_closest_u(S, o, d, stk, h, st);
@@ -567,6 +622,7 @@ RT_HD bool fast_query_closest(const RtSceneView& S, V3 o, V3 d, STK& stk, float&
         k_out = -1;
         return true;
     }
+    if (RT_FUZZ_CHECK && fuzzy_hit(S, h.k, o, d)) return false;
     if (S.brute) {  // USE_BVH 0: the closest M-T hit, lowest index on ties; no octree
         t_out = h.t;
         k_out = h.k;
@@ -588,6 +644,7 @@ RT_HD bool fast_query_closest(const RtSceneView& S, V3 o, V3 d, STK& stk, float&
 template <class STK, int WALK = RT_FAST_WALK_A>
 RT_HD int fast_query_any(const RtSceneView& S, V3 o, V3 d, STK& stk, Stats* st)
 {
+    if (far_origin(S, o)) return -1;
     if (WALK == 1) return fast_any_u(S, o, d, stk, st);
     if (st) st->c[RT_STAT_ANY_RAYS]++;
     if (rt_isnan(d.x) || rt_isnan(d.y) || rt_isnan(d.z) || rt_isnan(o.x) || rt_isnan(o.y) || rt_isnan(o.z)) return 0;

@@ -121,6 +121,8 @@ __device__ __forceinline__ QChild quad_child(const RtSceneView& S, int node, int
 
 // Lane `sub`'s triangle of a leaf item: Moller-Trumbore (the reference's
 // arithmetic). Returns t (+inf when the lane has no triangle or no hit).
+// MARK (closest-hit walks): a hit fuzzier than its box pad marks its leaf (below).
+template <bool MARK>
 __device__ __forceinline__ float quad_tri(const RtSceneView& S, int item, int sub, V3 o, V3 d, int& k, int& leaf,
                                           int& prim)
 {
@@ -140,7 +142,11 @@ __device__ __forceinline__ float quad_tri(const RtSceneView& S, int item, int su
         if (tri_test_v(ld3(a), ld3(e1), ld3(e2), o, d, t)) {
             tv = t;
             k = (int)rt_asuint(a.w);
-            leaf = (int)rt_asuint(e1.w);
+            // (RT_FUZZ_CHECK builds: a hit fuzzier than its box pad marks its leaf, and the
+            // walk's answer then goes to the exact walk, quad_closest_answer; the mark travels
+            // with the leaf through the reductions, and a same-leaf tie of marked and unmarked
+            // hits counts as mixed)
+            leaf = (int)rt_asuint(e1.w) | (RT_FUZZ_CHECK && MARK && fuzzy_tri(a, e1, e2, o, d) ? RT_FZ_BIT : 0);
             prim = (int)rt_asuint(e2.w);
         }
     }
@@ -365,7 +371,7 @@ __device__ __forceinline__ int quad_visit(const RtSceneView& S, QState& q, QSTK&
     if (q.cur < 0) {
         if (st && sub == 0) st->c[ANY ? RT_STAT_ANY_TRI : RT_STAT_TRI] += ((~q.cur) & 3) + 1;
         int k, leaf, prim;
-        const float tv = quad_tri(S, q.cur, sub, q.o, q.d, k, leaf, prim);
+        const float tv = quad_tri<!ANY>(S, q.cur, sub, q.o, q.d, k, leaf, prim);
         if (ANY) {
             const int hitb = tv < __builtin_inff() ? 1 : 0;
             if (S.brute) {
@@ -455,6 +461,8 @@ __device__ __forceinline__ bool quad_closest_answer(const RtSceneView& S, const 
         k_out = -1;
         return true;
     }
+    // the found hit fuzzier than its box pad (rt_fast.h fuzzy_tri, marked by quad_tri)
+    if (RT_FUZZ_CHECK && (h.leaf & RT_FZ_BIT)) return false;
     if (S.brute) {
         t_out = h.t;
         k_out = h.k;

@@ -484,10 +484,11 @@ struct FastStack {
     }
 };
 
-// RT_FORCE_FALLBACK: does this query skip the quad walk (a schedule-independent hash of the ray)?
+// Does this query skip the search-BVH walk for the exact octree walk? Its origin lies outside
+// the near box (rt_fast.h far_origin), or the force_fallback stressor's ray hash selects it.
 __device__ __forceinline__ bool forced_fallback(const rtk::WaveView& W, const float4_& o, const float4_& d)
 {
-    return rtk::forced_fallback(W.force_fb, o, d);
+    return (W.far_check && rtk::far_origin(W.S, rtk::v3of(o))) || rtk::forced_fallback(W.force_fb, o, d);
 }
 
 // Blocks [0, n0) take role 0, the rest role 1, in proportion to the work.
@@ -1423,7 +1424,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, 8))) v
     for (int i = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 2); i < n; i += stride) {
         rtk::QState qs;
         int res = 1;
-        if (rtk::qstate_begin<ANY>(qs, rtk::v3of(rays[2 * i]), rtk::v3of(rays[2 * i + 1]), sub, nullptr))
+        if (rtk::far_origin(S, rtk::v3of(rays[2 * i])))
+            res = -1;  // (the exact walk's)
+        else if (rtk::qstate_begin<ANY>(qs, rtk::v3of(rays[2 * i]), rtk::v3of(rays[2 * i + 1]), sub, nullptr))
             do {
                 res = rtk::quad_visit<ANY>(S, qs, stk, sub, nullptr);
             } while (res == 0);
@@ -1454,7 +1457,9 @@ __global__ __launch_bounds__(256) void k_query_row(RtSceneView S, const float4_*
     for (int i = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 4); i < n; i += stride) {
         rtk::QState qs;
         int res = 1;
-        if (rtk::qstate_begin<ANY>(qs, rtk::v3of(rays[2 * i]), rtk::v3of(rays[2 * i + 1]), sub, nullptr))
+        if (rtk::far_origin(S, rtk::v3of(rays[2 * i])))
+            res = -1;  // (the exact walk's)
+        else if (rtk::qstate_begin<ANY>(qs, rtk::v3of(rays[2 * i]), rtk::v3of(rays[2 * i + 1]), sub, nullptr))
             do {
                 res = rtk::row_visit<ANY, RT_VISIT_DESCEND>(S, qs, stk, sub, nullptr);
             } while (res == 0);
@@ -1695,6 +1700,7 @@ int upload_one(rt_context* c, Backend* b, const std::vector<int32_t>& matk, bool
     v.parent = (const int32_t*)b->parent.p;
     v.leaf_of = (const int32_t*)b->leaf_of.p;
     v.tri_mat = 1;
+    rt_view_near(c, v);
     b->view = v;
     b->bl_rays = rt_scene_has_emissive_prim(c) ? 1 : 0;
     b->any_rays = v.n_spheres == 0 ? 1 : 0;
@@ -1706,7 +1712,9 @@ int rt_backend_create(rt_context* c)
 {
     Group* g = new Group();
     c->backend = g;
-    g->multi = c->devices.size() > 1;  // (one listed device: a single-device context on it)
+    // (one listed device: a single-device context on it, unless a test asks for the driver
+    // and a one-rank RCCL clique: rt_test_create_multi_rccl)
+    g->multi = c->devices.size() > 1 || (c->force_multi && !c->devices.empty());
     g->loopback = g->multi && c->loopback;
     const std::vector<int> ids = g->multi ? c->devices : std::vector<int>{c->device};
     for (int d : ids) {
@@ -1922,6 +1930,7 @@ int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounces, cons
         if (int r = ensure(c, b->wave[l], need)) return r;
         rtk::wave_carve((char*)b->wave[l].p, (size_t)La.n, W);
         W.S = b->view;
+        rt_view_near(c, W.S);  // (rt_test_schedule may have changed it since the upload)
         W.cam = c->cam;
         W.src = ls;
         W.W = w;

@@ -171,7 +171,7 @@ __device__ __forceinline__ int row_visit(const RtSceneView& S, QState& q, RSTK& 
         const int mine_leaf = g == 0 ? l0 : g == 1 ? l1 : g == 2 ? l2 : l3;
         int k = -1, leaf = -1, prim = 0x7fffffff;
         float tv = __builtin_inff();
-        if (g < nl) tv = quad_tri(S, mine_leaf, sub & 3, q.o, q.d, k, leaf, prim);
+        if (g < nl) tv = quad_tri<!ANY>(S, mine_leaf, sub & 3, q.o, q.d, k, leaf, prim);
         if (ANY) {
             unsigned hm = row_bits(__ballot(tv < __builtin_inff()));
             if (S.brute) {

@@ -978,6 +978,10 @@ constexpr int kBins = 16, kLeafMax = 4;
 // for its triangles (barycentric / t round-off ~1e-6 relative to coordinate
 // magnitudes) is strictly inside, and the traversal's float slab test on the
 // padded box cannot miss such a point.
+// (How far the reference's test reaches outside a triangle grows with the ray's distance and
+// its grazing angle, not with the coordinates: DESIGN.md §4 "Far origins and grazing hits".
+// A floor of 1e-4 x the scene's magnitude on every pad, 10x this one for the dragon's boxes,
+// cut the probe's near grazing misses only ~5x: profiles/r06_far_origin.json.)
 void pad_box(const Box& b, float* mn, float* mx)
 {
     float mag = 1.0f;

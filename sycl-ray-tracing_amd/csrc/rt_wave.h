@@ -71,6 +71,7 @@ struct WaveView {
     int W, H, spp, bounces;
     float cam_o[3];         // xform_point(cam, 0): every camera ray's origin (set_view_consts)
     float aspect;           // (float)W / (float)H
+    int far_check;          // the camera lies outside the near box: test every query's origin (rt_fast.h far_origin)
     int n_slots;
     int bl_rays;            // 0: no primitive has an emissive material -> BRDF->light rays can't contribute
     int any_rays;           // 1: occlusion queries may use the any-hit walk (no analytic spheres)
@@ -381,6 +382,9 @@ RT_HD void set_view_consts(WaveView& W)
     W.cam_o[1] = o.y;
     W.cam_o[2] = o.z;
     W.aspect = (float)W.W / (float)W.H;
+    // (a render whose camera lies in the near box casts every other ray from a surface of the
+    // scene, inside it too: its queries skip the per-query near-box test; W.S set before this)
+    W.far_check = far_origin(W.S, o) ? 1 : 0;
 }
 
 // Framebuffer entry of slot p: slot rows map to every fb_rs-th framebuffer row.

@@ -197,7 +197,8 @@ class RenderKernel:
 
     def __init__(self, width, height, render_samples, max_bounces, image_buffer: Image, triangle_buffer,
                  materials_buffer, emissive_triangle_indices_buffer, materials_indices_buffer, analytic_spheres_buffer,
-                 bvh: BVH, skysphere: Image, env_map_cdf, device=0, hostsim: bool = False, loopback: bool = False):
+                 bvh: BVH, skysphere: Image, env_map_cdf, device=0, hostsim: bool = False, loopback: bool = False,
+                 rccl_clique: bool = False):
         self.L = lib(hostsim)
         self.width, self.height = int(width), int(height)
         self.render_samples, self.max_bounces = int(render_samples), int(max_bounces)
@@ -206,7 +207,9 @@ class RenderKernel:
         if isinstance(device, (list, tuple)):
             # loopback (tests / rehearsals only): the list may repeat a GPU, shards move by device copies
             ids = np.ascontiguousarray(device, dtype=np.int32)
-            create = self.L.rt_create_multi_loopback if loopback else self.L.rt_create_multi
+            # rccl_clique (tests only): the RCCL driver even for one device (rt_test_create_multi_rccl)
+            create = (self.L.rt_create_multi_loopback if loopback else
+                      self.L.rt_test_create_multi_rccl if rccl_clique else self.L.rt_create_multi)
             check(self.L, create(ids.shape[0], ptr(ids), ctypes.byref(h)), None, "rt_create_multi")
         else:
             check(self.L, self.L.rt_create(int(device), ctypes.byref(h)), None, "rt_create")

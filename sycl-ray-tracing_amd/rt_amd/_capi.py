@@ -14,7 +14,7 @@ import os
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_DIR = os.path.join(PKG_DIR, "lib")
 PRODUCT = os.environ.get("RT_HIP_LIB") or os.path.join(LIB_DIR, "librt_hip.so")  # (override: debug builds)
-HOSTSIM = os.path.join(LIB_DIR, "librt_hostsim.so")
+HOSTSIM = os.environ.get("RT_HOSTSIM_LIB") or os.path.join(LIB_DIR, "librt_hostsim.so")  # (override: study builds)
 
 # every symbol declared in include/rt_hip.h (tests check the export table)
 EXPORTS = [
@@ -24,7 +24,7 @@ EXPORTS = [
     "rt_mesh_load", "rt_mesh_counts", "rt_mesh_copy", "rt_mesh_free", "rt_camera_preset", "rt_env_luminance_cdf",
     "rt_octree_dump", "rt_read_hdr", "rt_write_png", "rt_image_to_rgba8",
     "rt_set_intersect_mode", "rt_create_multi", "rt_device_count", "rt_set_materials", "rt_render_variants",
-    "rt_create_multi_loopback", "rt_test_fail_device", "rt_test_schedule", "rt_test_walk_log",
+    "rt_create_multi_loopback", "rt_test_create_multi_rccl", "rt_test_fail_device", "rt_test_schedule", "rt_test_walk_log",
     "rt_test_walk_log_read", "rt_test_obj_parallel_min",
 ]
 
@@ -40,6 +40,7 @@ _SIGS = {
     "rt_create": (I, [I, ctypes.POINTER(P)]),
     "rt_create_multi": (I, [I, P, ctypes.POINTER(P)]),
     "rt_create_multi_loopback": (I, [I, P, ctypes.POINTER(P)]),
+    "rt_test_create_multi_rccl": (I, [I, P, ctypes.POINTER(P)]),
     "rt_test_fail_device": (I, [P, I]),
     "rt_test_schedule": (I, [P, ctypes.c_char_p, ctypes.c_double]),
     "rt_test_walk_log": (I, [P, I, I, I]),

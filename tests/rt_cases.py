@@ -66,7 +66,7 @@ def golden_case(name: str, manifest: dict) -> dict:
 
 
 def make_kernel(entry: dict, cameras: dict, hostsim: bool, W=None, H=None, spp=None, bounces=None, fb=None,
-                spheres=None, device=0, materials=None, loopback=False):
+                spheres=None, device=0, materials=None, loopback=False, rccl_clique=False):
     P = parsed_scene(entry["scene"])
     W = W or entry["W"]
     H = H or entry["H"]
@@ -79,7 +79,7 @@ def make_kernel(entry: dict, cameras: dict, hostsim: bool, W=None, H=None, spp=N
     rk = rt_amd.RenderKernel(W, H, spp or entry["spp"], bounces or entry["bounces"], fb, P.triangles,
                              mats, P.emissive_triangle_indices, mi, spheres,
                              rt_amd.BVH(P.triangles), rt_amd.Image.from_rgb(sky(entry["sky"])), None,
-                             hostsim=hostsim, device=device, loopback=loopback)
+                             hostsim=hostsim, device=device, loopback=loopback, rccl_clique=rccl_clique)
     rk.set_camera(rt_amd.Camera(c[:16], c[16]))
     return rk, fb
 

@@ -72,4 +72,6 @@ def test_gpu_row_walks_match_quad_walks_and_octree():
         ex = rk.intersect(rays[ok][:, [0, 1, 2, 4, 5, 6]])
         np.testing.assert_array_equal(np.where(ex[:, 0] == 1, ex[:, 2].view(np.float32), -1.0).astype(np.float32)
                                       .view(np.uint32), tr[ok].view(np.uint32), err_msg=f"{name}: vs octree")
+        # ... and the triangle (rows and quads settle same-leaf ties the way the octree walk does)
+        np.testing.assert_array_equal(np.where(ex[:, 0] == 1, ex[:, 1], -1), kr[ok], err_msg=f"{name}: k vs octree")
     assert seen_unoccluded

@@ -142,6 +142,46 @@ def test_gpu_multi_context_one_device_is_single(manifest, cameras):
 
 
 @pytest.mark.gpu
+def test_gpu_multi_device_driver_rccl_one_rank(manifest, cameras):
+    """The RCCL path itself on one GPU (rt_test_create_multi_rccl([0]): a one-rank
+    ncclCommInitAll clique): render_multi's pack, ncclScatter of the caller's framebuffer
+    rows, the device's wavefront loop into its block, ncclGather back to the root and the
+    un-permute (render_kernel.cpp:169-180, 189-211), bit-identical to the goldens for the
+    Cornell frame and row shards, and to the single-device context for a dragon row shard."""
+    from hip_mem import DeviceBuffer
+    e = rt_cases.golden_case("cornell32_128", manifest)
+    rk, fb = rt_cases.make_kernel(e, cameras, hostsim=False, device=[0], rccl_clique=True)
+    assert rk.n_devices == 1
+    rk.render()
+    np.testing.assert_array_equal(_bits(fb.pixels), _bits(e["expected"]))
+    for off, stride in ((0, 1), (1, 3)):
+        rows = len(range(off, e["H"], stride))
+        init = np.zeros((rows, e["W"], 4), np.float32)
+        init[..., 3] = 1.0
+        buf = DeviceBuffer(init.nbytes)
+        buf.upload(init)
+        rk.render_device(buf.ptr, off, stride, None)
+        got = buf.download(init.shape, np.float32)
+        np.testing.assert_array_equal(_bits(got), _bits(e["expected"][off::stride]))
+    c1 = rt_cases.golden_case("cfg1_cornell12", manifest)
+    rk1, fb1 = rt_cases.make_kernel(c1, cameras, hostsim=False, device=[0], rccl_clique=True)
+    rk1.render()
+    np.testing.assert_array_equal(_bits(fb1.pixels), _bits(c1["expected"]))
+    g = rt_cases.golden_case("cfg2_dragon", manifest)
+    rkr, _ = rt_cases.make_kernel(g, cameras, hostsim=False, device=[0], spp=4, rccl_clique=True)
+    rks, _ = rt_cases.make_kernel(g, cameras, hostsim=False, device=0, spp=4)
+    outs = []
+    for k in (rkr, rks):
+        rows = len(range(3, g["H"], 5))
+        init = np.zeros((rows, g["W"], 4), np.float32)
+        buf = DeviceBuffer(init.nbytes)
+        buf.upload(init)
+        k.render_device(buf.ptr, 3, 5, None)
+        outs.append(buf.download(init.shape, np.float32))
+    np.testing.assert_array_equal(_bits(outs[0]), _bits(outs[1]))
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("ids", [[0, 0], [0, 0, 0]])
 def test_gpu_multi_device_driver_loopback(ids, manifest, cameras):
     """The multi-device driver on one GPU (rt_create_multi_loopback: the device list may name
