@@ -149,7 +149,7 @@ RtSceneView rt_host_view(const rt_context* ctx);  // host-memory view (hostsim)
 // widened on every side by RT_NEAR_SCALE (or sched.near_scale) x the box's largest extent;
 // unbounded for an empty scene.
 #ifndef RT_NEAR_SCALE
-#define RT_NEAR_SCALE 1.0
+#define RT_NEAR_SCALE 0.5
 #endif
 void rt_view_near(const rt_context* ctx, RtSceneView& v);
 // Does any primitive (triangle or sphere) use a material with a positive

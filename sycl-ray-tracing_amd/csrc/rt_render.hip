@@ -172,6 +172,7 @@ struct Backend {
     int32_t* h_hist[RT_MAX_LANES] = {};
     rtk::WaveView* h_fviews = nullptr;  // pinned
     hipEvent_t fev[RT_MAX_LANES] = {}, fev_done = nullptr;
+    hipEvent_t hev[RT_MAX_LANES] = {};  // fast lane: each lane's samples-done histogram readback
     bool fev_done_recorded = false;
     hipEvent_t ftev[2] = {};  // (timed renders: around the fast lane's kernel)
     hipStream_t fs = nullptr;  // the fast lane's stream with 4 lanes (fewer: the first idle lane stream)
@@ -1610,6 +1611,7 @@ void destroy_one(Backend* b)
     for (int l = 0; l < RT_MAX_LANES; l++) {
         if (b->h_hist[l]) (void)hipHostFree(b->h_hist[l]);
         if (b->fev[l]) (void)hipEventDestroy(b->fev[l]);
+        if (b->hev[l]) (void)hipEventDestroy(b->hev[l]);
     }
     if (b->h_fviews) (void)hipHostFree(b->h_fviews);
     if (b->fev_done) (void)hipEventDestroy(b->fev_done);
@@ -1796,7 +1798,8 @@ struct WaveLane {
     long live = 0;  // live paths at the last readback (an upper bound: paths only finish)
     bool done = false, tail_next = false;
     int await = 0;  // 0 none, 1 live count, 2 fallback counts (tail entry check)
-    int fast_state = 0;  // fast lane: 0 waiting, 1 hand-over at the next k_step, 2 handed over, 3 none
+    int fast_state = 0;  // fast lane: 0 waiting, 4 threshold read back (pending), 1 hand-over at the
+                         // next k_step, 2 handed over, 3 none
     int fast_thr = 0, fast_n = 0;  // ... samples-done threshold, paths at most
     hipEvent_t (*tev)[RT_MAX_TIMED_ITERS] = nullptr;  // [3][RT_MAX_TIMED_ITERS]
 };
@@ -1958,6 +1961,7 @@ int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounces, cons
             if (int r = ensure(c, b->fspill[l], (size_t)((La.fast_n + 3) / 4) * threads * RT_STACK_CAP * 8)) return r;
             if (!b->h_hist[l]) HIPCHK(c, hipHostMalloc((void**)&b->h_hist[l], (RT_FAST_MAX_SPP + 1) * 4, hipHostMallocDefault));
             if (!b->fev[l]) HIPCHK(c, hipEventCreateWithFlags(&b->fev[l], hipEventDisableTiming));
+            if (!b->hev[l]) HIPCHK(c, hipEventCreateWithFlags(&b->hev[l], hipEventDisableTiming));
             HIPCHK(c, hipMemsetAsync(b->fcnt[l].p, 0, C_COUNT * sizeof(int32_t), La.s));
         }
         W.iterq = (S && iter_log && l == 0) ? (int32_t*)b->iterq.p : nullptr;
@@ -2025,7 +2029,7 @@ int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounces, cons
         if (fast_k == 0 || fast_launched) return RT_OK;
         bool any = false;
         for (int l = 0; l < nl; l++) {
-            if (L[l].fast_state < 2) return RT_OK;
+            if (L[l].fast_state < 2 || L[l].fast_state == 4) return RT_OK;  // (a lane still to hand over)
             any = any || L[l].fast_state == 2;
         }
         fast_launched = true;
@@ -2074,9 +2078,30 @@ int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounces, cons
         b->fev_done_recorded = fast_ran = true;
         return RT_OK;
     };
+    // the fast lane's threshold: the samples-done count of the lane's fast_n-th slowest live
+    // path, from the histogram k_hist read back (polled: the host thread serving every lane
+    // never blocks on it; the hand-over happens at the first k_step after it has landed)
+    auto fast_threshold = [&](WaveLane& La) -> int {
+        const int l = (int)(&La - L);
+        const hipError_t q = hipEventQuery(b->hev[l]);
+        if (q == hipErrorNotReady) return RT_OK;
+        HIPCHK(c, q);
+        long acc = 0;
+        int thr = spp;
+        for (int k = 0; k <= spp; k++)
+            if ((acc += b->h_hist[l][k]) >= La.fast_n) {
+                thr = k;
+                break;
+            }
+        La.fast_thr = thr;
+        La.fast_state = 1;
+        return RT_OK;
+    };
     auto launch_step = [&](WaveLane& La) -> int {
         const int par = La.it & 1;
         const int l = (int)(&La - L);
+        if (La.fast_state == 4)
+            if (int r = fast_threshold(La)) return r;
         const bool hand = La.fast_state == 1;
         int32_t* fl = (int32_t*)b->fast[l].p;
         if (hand) {  // this step hands the lane's slowest paths to the fast lane
@@ -2160,11 +2185,13 @@ int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounces, cons
         La.live = live;
         La.done = live == 0;
         La.tail_next = !La.done && live <= tail_max;
-        if (La.fast_state == 0 && (La.done || La.tail_next)) {  // (no hand-over from this lane)
+        if ((La.fast_state == 0 || La.fast_state == 4) && (La.done || La.tail_next)) {  // (no hand-over from this lane)
+            if (La.fast_state == 4) HIPCHK(c, hipEventSynchronize(b->hev[(int)(&La - L)]));  // (its readback is done with h_hist)
             La.fast_state = 3;
             if (int r = fast_launch()) return r;
         } else if (La.fast_state == 0 && La.it >= fast_iter) {
-            // the threshold: the samples-done count of the lane's fast_n-th slowest live path
+            // the samples-done histogram of the lane's live paths, read back asynchronously
+            // (fast_threshold picks it up from a later k_step launch)
             const int l = (int)(&La - L);
             int32_t* hh = (int32_t*)b->fhist[l].p;
             HIPCHK(c, hipMemsetAsync(hh, 0, (size_t)(spp + 1) * 4, La.s));
@@ -2174,16 +2201,8 @@ int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounces, cons
                                La.s, HW, La.it & 1, hh);
             HIPCHK(c, hipGetLastError());
             HIPCHK(c, hipMemcpyAsync(b->h_hist[l], hh, (size_t)(spp + 1) * 4, hipMemcpyDeviceToHost, La.s));
-            HIPCHK(c, hipStreamSynchronize(La.s));
-            long acc = 0;
-            int thr = spp;
-            for (int k = 0; k <= spp; k++)
-                if ((acc += b->h_hist[l][k]) >= La.fast_n) {
-                    thr = k;
-                    break;
-                }
-            La.fast_thr = thr;
-            La.fast_state = 1;
+            HIPCHK(c, hipEventRecord(b->hev[l], La.s));
+            La.fast_state = 4;
         }
         return RT_OK;
     };

@@ -41,9 +41,9 @@ def _want(g):
     return t, k
 
 
-def _near(scene, o, scale=1.0):
+def _near(scene, o, scale=0.5):
     """Origins inside the near box (rt_view_near: the scene's box widened on every side by
-    scale x its largest extent; RT_NEAR_SCALE 1), with a 1e-3 guard band either way."""
+    scale x its largest extent; RT_NEAR_SCALE 0.5), with a 1e-3 guard band either way."""
     v = np.asarray(parsed_scene(scene).triangles, np.float64).reshape(-1, 3)
     lo, hi = v.min(0), v.max(0)
     w = scale * (hi - lo).max()

@@ -34,7 +34,7 @@ from gen_golden_brute import run  # noqa: E402
 REF = os.path.join(gio.REPO, "oracle", "_ref", "ref_driverO2")
 OUT = gio.GOLDEN
 N_PER = 512
-DISTS = {"cornell": [3.0, 10.0, 1e2, 1e3, 1e4, 1e5], "dragon": [20.0, 50.0, 1e2, 1e3, 1e4, 1e5]}
+DISTS = {"cornell": [1.0, 2.0, 1e2, 1e3, 1e4, 1e5], "dragon": [10.0, 20.0, 1e2, 1e3, 1e4, 1e5]}
 # (name, scene, sky, camera spec, W, H, spp, bounces)
 RENDERS = [
     ("cornell_tele", "cornell", "S", "tele:0.0475:0:0:1:3500", 64, 64, 2, 3),
