@@ -72,6 +72,11 @@ build/walk_probe: tools/probe/walk_probe.cpp $(OBJ)/rt_scene.host.o $(HDRS)
 	@mkdir -p build
 	$(CXX) -std=c++17 -O2 -fopenmp -ffp-contract=off -I$(SRC) $< $(OBJ)/rt_scene.host.o -o $@ -lpthread
 
+# CPU trip counts of stackless occlusion walks vs the short stack (tools/probe/stackless_probe.cpp; study tool)
+build/stackless_probe: tools/probe/stackless_probe.cpp $(OBJ)/rt_scene.host.o $(HDRS)
+	@mkdir -p build
+	$(CXX) -std=c++17 -O2 -fopenmp -ffp-contract=off -I$(SRC) $< $(OBJ)/rt_scene.host.o -o $@ -lpthread
+
 # the reference build (container only; needs /root/reference)
 ref:
 	$(MAKE) -C oracle/ref OPT=-O2
