@@ -106,8 +106,9 @@ RT_HD float rt_half(uint32_t h)
 // Oriented slab of a search-BVH child (rt_scene.cpp build_slabs): s = {normal x | y << 16 and
 // z as f16 bits, lo, hi}. The ray's segment [max(t0, 0), t1] inside the child's box can only
 // reach a triangle of the child if it meets {lo <= n.x <= hi}; false when the whole segment
-// lies on one side. Conservative: the host's margin covers this f32 arithmetic for any ray
-// inside the scene's box; a child without a slab has n = 0, lo = -inf, hi = +inf
+// lies on one side. Conservative: the host's margin covers this f32 arithmetic for a ray
+// whose origin lies in the near box (far_origin below; DESIGN.md §4 "Far origins and grazing
+// hits"), the only rays the search BVH answers; a child without a slab has n = 0, lo = -inf, hi = +inf
 // (and a NaN from inf * 0 only drops that endpoint: fmin / fmax).
 #ifndef RT_SLABS
 #define RT_SLABS 1

@@ -1371,9 +1371,10 @@ static uint16_t f16_bits(float f)
 // area-weighted mean normal n (when the normals do not cancel: |sum| > half the summed
 // areas) quantized to f16 gives the slab {x : lo <= n.x <= hi} over the run's vertices
 // a, a + e1, a + e2 (exactly the triangle Moller-Trumbore tests), widened by a margin that
-// covers the kernel's f32 evaluation of n.o + t n.d along any ray inside the scene's box and
-// the Moller-Trumbore hit's distance from its triangle's plane (~2e-6 of the
-// scene's magnitude; the margin is 1e-4 of the child's magnitude + 1e-5 of the scene's).
+// covers the kernel's f32 evaluation of n.o + t n.d along a ray from the near box (the scene's
+// box + 0.5 x its largest extent: queries from farther take the exact walk, rt_fast.h
+// far_origin) and the Moller-Trumbore hit's distance from its triangle's plane (DESIGN.md §4:
+// ~eps |o - a| off the plane; the margin is 1e-4 of the child's magnitude + 1e-5 of the scene's).
 // A ray segment inside the child's box that lies entirely on one side of the slab cannot
 // reach a hit there: such children are not entered. Grazing rays above a curved tessellated
 // surface enter many boxes but few slabs (the long search-BVH walks, profiles/r05_walk_*).
