@@ -283,8 +283,8 @@ __host__ __device__ __forceinline__ size_t qbase(bool heavy, int shard, size_t s
 // parity pout, in the shard of the 64-item input chunk `base` (whole wave).
 // Shards take contiguous runs of the n_in inputs' chunks, so a queue read in
 // order follows its input order (pixel order, through the compactions).
-__device__ __forceinline__ void append_emit(const rtk::WaveView& W, int pout, int base, int n_in, int p,
-                                            const rtk::Emit& e)
+template <class E>
+__device__ __forceinline__ void append_emit(const rtk::WaveView& W, int pout, int base, int n_in, int p, const E& e)
 {
     const int cps = ((n_in + 63) / 64 + RT_QSHARDS - 1) / RT_QSHARDS;  // chunks per shard
     const int sh = min(RT_QSHARDS - 1, (base >> 6) / cps);
@@ -438,6 +438,9 @@ __global__ __launch_bounds__(256) void k_tonemap(rtk::WaveView W)
 //    query whose answer needs the exact walk (or whose stack would overflow)
 //    goes to the fallback list for the next launch, and its slot's r_park
 //    count keeps k_step off the path until the walk has finished.
+#ifndef RT_STEP_EMIT_LDS
+#define RT_STEP_EMIT_LDS 1  // k_step's and k_tail's emitted rays wait in LDS (rt_wave.h EmitLds), not in VGPRs
+#endif
 #define RT_LDS_WORDS 16         // LDS words per lane of k_trace (16 KB per block of 256)
 #define RT_LDS_CAP_FAST 16      // search-BVH stack: node + key in LDS ...
 #define RT_SPILL_FAST RT_FAST_SPILL  // ... then in the lane's global spill area
@@ -719,7 +722,9 @@ __device__ void exact_any(const rtk::WaveView& W, int par, uint32_t* lds, int la
 template <bool STATS>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_STEP_OCC, 8))) void k_step(rtk::WaveView W, int par, unsigned long long* stats)
 {
-    __shared__ uint32_t s_lds[RT_LDS_WORDS * 256];
+    // (the exact roles' stacks; in the path-step blocks, the emitted rays: rt_wave.h EmitLds)
+    __shared__ uint32_t s_lds[(RT_STEP_EMIT_LDS ? 6 * rtk::RK_COUNT : RT_LDS_WORDS) * 256];
+    static_assert(6 * rtk::RK_COUNT >= RT_LDS_WORDS, "the exact roles' stacks fit the emit columns");
     __shared__ int s_pre[RT_QSHARDS + 1];
     rtlibm::lds_tables_init();
     rtk::lds_shade_init(W.S);  // (the env-map row search and a small material table from LDS)
@@ -769,7 +774,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_STEP_OCC
     const int wn = nbs * (int)(blockDim.x >> 6);
     for (int base = wg * 64; base < n; base += wn * 64) {
         const int idx = base + lane_id();
+#if RT_STEP_EMIT_LDS
+        rtk::EmitLds<256> e;
+        e.s = reinterpret_cast<float*>(s_lds) + threadIdx.x;
+#else
         rtk::Emit e;
+#endif
         e.mask = 0;
         e.active = false;
         e.heavy = false;
@@ -1106,6 +1116,45 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_OC
 // walk, so every path is ready to step; a query the quad walk cannot answer
 // is answered here by the exact walk, inline, by lane 0 of its quad.
 #define RT_TAIL_MAXP 16  // paths per wave at most (RK_COUNT rays each per list)
+#ifndef RT_TAIL_EMIT_LDS
+#define RT_TAIL_EMIT_LDS RT_STEP_EMIT_LDS
+#endif
+#if RT_TAIL_EMIT_LDS
+// k_tail: a path's emitted rays stay in the wave's LDS columns (EmitLds<RT_TAIL_MAXP>, lane j
+// of the wave's paths in column j); the lists hold (j << 3 | kind) (l0: closest-hit kinds,
+// l1: occlusion)
+using TailEmit = rtk::EmitLds<RT_TAIL_MAXP>;
+__device__ __forceinline__ void tail_lists(const TailEmit& e, int last_kind, uint8_t* l0, uint8_t* l1, int* nl)
+{
+    const int lane = lane_id();
+    nl[0] = nl[1] = 0;
+#pragma unroll
+    for (int k = 0; k < rtk::RK_COUNT; k++) {
+        const bool want = (e.mask >> k) & 1u;
+        const unsigned long long b = __ballot(want);
+        const int l = k <= last_kind ? 0 : 1;
+        if (want) (l ? l1 : l0)[nl[l] + __popcll(b & ((1ull << lane) - 1ull))] = (uint8_t)((lane << 3) | k);
+        nl[l] += __popcll(b);
+    }
+}
+// k_tail's path step (lanes with my >= 0) and list append, out of line (its registers apart
+// from the walk loop's; inlined, the tail loop spilled across every step: cfg2 811 -> 828
+// Msamples/s, cfg4 8-way shard 436 -> 403 ms, r02): bit 0 the lane's path stays in
+// flight, bits 1-10 / 11- the closest / occlusion list lengths.
+__device__ __noinline__ int tail_step(const rtk::WaveView& W, int my, int last_kind, float* cols, uint8_t* l0, uint8_t* l1,
+                                      rtk::Stats* ps)
+{
+    TailEmit e;
+    e.s = cols + (lane_id() & (RT_TAIL_MAXP - 1));  // (lanes >= W.tail_paths never step)
+    e.mask = 0;
+    e.active = false;
+    e.heavy = false;
+    if (my >= 0) rtk::path_step(W, my, e, ps);
+    int nl[2];
+    tail_lists(e, last_kind, l0, l1, nl);
+    return (e.active ? 1 : 0) | (nl[0] << 1) | (nl[1] << 11);
+}
+#else
 // k_tail: a path's emitted rays -> the wave's LDS lists (l0: closest-hit kinds, l1: occlusion)
 __device__ __forceinline__ void tail_lists(const rtk::Emit& e, int slot, int last_kind, rtk::RayRec* l0, rtk::RayRec* l1,
                                            int* nl)
@@ -1124,10 +1173,7 @@ __device__ __forceinline__ void tail_lists(const rtk::Emit& e, int slot, int las
         nl[l] += __popcll(b);
     }
 }
-// k_tail's path step (lanes with my >= 0) and list append, out of line (its registers apart
-// from the walk loop's; inlined, the tail loop spilled across every step: cfg2 811 -> 828
-// Msamples/s, cfg4 8-way shard 436 -> 403 ms, r02): bit 0 the lane's path stays in
-// flight, bits 1-10 / 11- the closest / occlusion list lengths.
+// (as above, the rays in registers and the lists of whole records)
 __device__ __noinline__ int tail_step(const rtk::WaveView& W, int my, int last_kind, rtk::RayRec* l0, rtk::RayRec* l1,
                                       rtk::Stats* ps)
 {
@@ -1140,6 +1186,7 @@ __device__ __noinline__ int tail_step(const rtk::WaveView& W, int my, int last_k
     tail_lists(e, my, last_kind, l0, l1, nl);
     return (e.active ? 1 : 0) | (nl[0] << 1) | (nl[1] << 11);
 }
+#endif
 // k_tail's inline exact walk (a query the quad walk cannot settle: ~1e-6 of them), kept
 // out of line so that its registers do not add to the tail loop's: inlined, k_tail
 // needed 468 VGPR spill slots at its 168-VGPR budget, out of line ~190.
@@ -1173,7 +1220,13 @@ __device__ __noinline__ void tail_exact(const rtk::WaveView& W, int l, uint32_t 
 template <bool STATS, bool PAIR, int G, bool FAST>
 __device__ __forceinline__ void tail_body(const rtk::WaveView& W, int par, unsigned long long* stats, int blk)
 {
+#if RT_TAIL_EMIT_LDS
+    __shared__ float s_em[4][6 * rtk::RK_COUNT * RT_TAIL_MAXP];        // per wave: its paths' rays (TailEmit columns)
+    __shared__ uint8_t s_q[4][2][RT_TAIL_MAXP * rtk::RK_COUNT];        // per wave: closest list, occlusion list
+    __shared__ int s_my[4][RT_TAIL_MAXP];                              // per wave: the slot of column j
+#else
     __shared__ rtk::RayRec s_q[4][2][RT_TAIL_MAXP * rtk::RK_COUNT];  // per wave: closest list, occlusion list
+#endif
     __shared__ uint32_t s_stk[2 * RT_QSTACK * 64];
     __shared__ int s_pre[RT_QSHARDS + 1];
     rtlibm::lds_tables_init();
@@ -1227,7 +1280,12 @@ __device__ __forceinline__ void tail_body(const rtk::WaveView& W, int par, unsig
         const long long t0 = probe ? wall_clock64() : 0;
         int nl[2];
         {
+#if RT_TAIL_EMIT_LDS
+            if (lane < RT_TAIL_MAXP) s_my[wv][lane] = my;
+            const int r = tail_step(W, my, last_kind, s_em[wv], s_q[wv][0], s_q[wv][1], ps);
+#else
             const int r = tail_step(W, my, last_kind, s_q[wv][0], s_q[wv][1], ps);
+#endif
             if (!(r & 1)) my = -1;
             nl[0] = (r >> 1) & 0x3ff;
             nl[1] = r >> 11;
@@ -1256,8 +1314,18 @@ __device__ __forceinline__ void tail_body(const rtk::WaveView& W, int par, unsig
                 const int qi = next + __popcll(bidle & ((1ull << (lane & ~(G - 1))) - 1ull));  // this group's query
                 if (!act && qi < nq) {
                     l = qi < nl[0] ? 0 : 1;
+#if RT_TAIL_EMIT_LDS
+                    const int ent = s_q[wv][l][l ? qi - nl[0] : qi], j = ent >> 3, kind = ent & 7;
+                    TailEmit ce;
+                    ce.s = s_em[wv] + j;
+                    rtk::RayRec r;
+                    r.o = rtk::f4(ce.o(kind), 0.0f);
+                    r.d = rtk::f4(ce.d(kind), 0.0f);
+                    target = ((uint32_t)s_my[wv][j] << 3) | (uint32_t)kind;
+#else
                     const rtk::RayRec r = s_q[wv][l][l ? qi - nl[0] : qi];
                     target = rt_asuint(r.d.w);
+#endif
                     q.o = rtk::v3of(r.o);
                     q.d = rtk::v3of(r.d);
                     if (forced_fallback(W, r.o, r.d)) {

@@ -230,6 +230,42 @@ RT_HD void emit(Emit& e, int kind, int slot, V3 o, V3 d)
     e.mask |= 1u << kind;
 }
 
+// k_step's and k_tail's Emit: the rays wait in LDS (this lane's column s: component c of
+// kind k at s[(6 k + c) * ST], ST lanes side by side, so a wave's lanes touch consecutive
+// words), not in up to 36 VGPRs held from the first emit through the rest of the shading
+// code to the append.
+template <int ST>
+struct EmitLds {
+    float* s;
+    uint32_t mask;
+    bool active;
+    bool heavy;
+    RT_HD V3 o(int kind) const { return v3(s[(6 * kind) * ST], s[(6 * kind + 1) * ST], s[(6 * kind + 2) * ST]); }
+    RT_HD V3 d(int kind) const { return v3(s[(6 * kind + 3) * ST], s[(6 * kind + 4) * ST], s[(6 * kind + 5) * ST]); }
+    RT_HD RayRec rec(int kind, int slot, float dw = 0.0f) const
+    {
+        const V3 ro = o(kind), rd = d(kind);
+        RayRec r;
+        r.o = float4_{ro.x, ro.y, ro.z, rt_asfloat((uint32_t)slot)};
+        r.d = float4_{rd.x, rd.y, rd.z, dw};
+        return r;
+    }
+};
+
+template <int ST>
+RT_HD void emit(EmitLds<ST>& e, int kind, int slot, V3 o, V3 d)
+{
+    (void)slot;
+    float* c = e.s + 6 * kind * ST;
+    c[0] = o.x;
+    c[ST] = o.y;
+    c[2 * ST] = o.z;
+    c[3 * ST] = d.x;
+    c[4 * ST] = d.y;
+    c[5 * ST] = d.z;
+    e.mask |= 1u << kind;
+}
+
 RT_HD V3 xform_point(const RtCamera& c, V3 p)  // mat.cpp:94-111
 {
     const float* m = c.m;
@@ -319,7 +355,8 @@ RT_HD void camera_ray(const WaveView& W, int x, int y, Rng& rng, V3& o, V3& d)
 // first hit at once: one step per sample fewer on the path's dependent chain. When
 // the continuation hits instead, the camera answer is dropped. The ray is computed
 // again, bit for bit the same, when its sample starts (begin_sample_ahead).
-RT_HD void next_camera(const WaveView& W, int p, const PathReg& P, Emit& e, uint32_t& fl)
+template <class E>
+RT_HD void next_camera(const WaveView& W, int p, const PathReg& P, E& e, uint32_t& fl)
 {
     if (!W.spec_cam || P.sample + 1 >= W.spp) return;
     // spec_cam 2: where the sample may go on (a continuation is cast), only at the bounce
@@ -338,7 +375,8 @@ RT_HD void next_camera(const WaveView& W, int p, const PathReg& P, Emit& e, uint
 // :56-73). Returns false when the pixel is complete (then fb is written).
 // With max_bounces == 0 the reference's bounce loop never runs: each sample
 // only draws its 2 jitter values and adds black.
-RT_HD bool start_sample(const WaveView& W, int p, PathReg& P, Emit& e)
+template <class E>
+RT_HD bool start_sample(const WaveView& W, int p, PathReg& P, E& e)
 {
     int x, y;
     pix_xy(W.src, p, x, y);
@@ -502,7 +540,8 @@ RT_HD bool hit_from(const RtSceneView& S, V3 o, V3 d, float t, int k, Hit& h)
 // with every RNG draw in the reference's order. Candidate contributions
 // are computed now (they depend only on the draws); resolve() decides with
 // the query results whether they count.
-RT_HD void shade(const WaveView& W, int p, PathReg& P, const Hit& h, Emit& e, Stats* st)
+template <class E>
+RT_HD void shade(const WaveView& W, int p, PathReg& P, const Hit& h, E& e, Stats* st)
 {
     const RtSceneView& S = W.S;
     if (st) st->c[RT_STAT_MAT]++;
@@ -720,7 +759,8 @@ RT_HD void resolve(const WaveView& W, int p, PathReg& P, const ResolveRec& R, St
 // (next_camera), is consumed in the same step (shaded, or that sample ends too and
 // the next camera ray is cast), else its camera ray is cast. Fills `e` with the rays
 // for the next trace.
-RT_HD void path_step(const WaveView& W, int p, Emit& e, Stats* st)
+template <class E>
+RT_HD void path_step(const WaveView& W, int p, E& e, Stats* st)
 {
     e.mask = 0;
     e.active = true;

@@ -25,6 +25,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstring>
 #include <random>
 #include <string>
 #include <vector>
@@ -109,6 +110,73 @@ struct Walker {
             cur = st.back();
             st.pop_back();
         }
+    }
+    // closest-hit walk with the quad walk's rule (rt_quad.h: nearest hit child next, the rest
+    // on the stack by entry distance, entries beyond t*(1 + RT_T2_WINDOW) dropped), started at
+    // node `start`; then (ancestor start) for every ancestor of `start` up to the root one more
+    // trip tests that ancestor's other children against the window and walks the ones hit.
+    // Returns trips; t_out = the closest M-T t (-1 none).
+    long closest_walk(V3 o, V3 d, int start, float& t_out) const
+    {
+        const rtk::RayB rb = rtk::rayb_setup(o, d);
+        float best = __builtin_inff();
+        long trips = 0;
+        std::vector<std::pair<float, int>> st;  // (entry, item)
+        auto window = [&]() { return best + best * RT_T2_WINDOW; };
+        auto walk_from = [&](int item) {
+            int cur = item;
+            for (;;) {
+                trips++;
+                if (cur >= 0) {
+                    const rtk::Bvh4R n = rtk::load_bvh4(S.bvh4, cur);
+                    float tn[4];
+                    bool h[4];
+                    rtk::box4(S, cur, n, rb, o, d, window(), tn, h);
+                    std::vector<std::pair<float, int>> hit;
+                    for (int c = 0; c < 4; c++)
+                        if (h[c] && tn[c] <= window())
+                            hit.push_back({tn[c], n.cnt[c] > 0 ? ~((n.ref[c] << 3) | n.cnt[c]) : n.ref[c]});
+                    std::sort(hit.begin(), hit.end());
+                    for (int j = (int)hit.size() - 1; j >= 1; j--) st.push_back(hit[j]);
+                    if (!hit.empty()) {
+                        cur = hit[0].second;
+                        continue;
+                    }
+                } else {
+                    const int v = ~cur;
+                    for (int j = 0; j < (v & 7); j++) {
+                        const float4_* r = S.bvh_tri4 + 3 * (size_t)((v >> 3) + j);
+                        float t;
+                        if (rtk::tri_test_v(rtk::ld3(r[0]), rtk::ld3(r[1]), rtk::ld3(r[2]), o, d, t)) best = std::min(best, t);
+                    }
+                }
+                cur = INT32_MIN;
+                while (!st.empty()) {
+                    const auto e = st.back();
+                    st.pop_back();
+                    if (e.first <= window()) {
+                        cur = e.second;
+                        break;
+                    }
+                }
+                if (cur == INT32_MIN) return;
+            }
+        };
+        walk_from(start);
+        for (int a = start; a != 0; a = parent[a]) {  // the ancestors' other children
+            const int p = parent[a];
+            trips++;
+            const rtk::Bvh4R n = rtk::load_bvh4(S.bvh4, p);
+            float tn[4];
+            bool h[4];
+            rtk::box4(S, p, n, rb, o, d, window(), tn, h);
+            for (int c = 0; c < 4; c++) {
+                if (c == slot[a] || !h[c] || !(tn[c] <= window())) continue;
+                walk_from(n.cnt[c] > 0 ? ~((n.ref[c] << 3) | n.cnt[c]) : n.ref[c]);
+            }
+        }
+        t_out = best == __builtin_inff() ? -1.0f : best;
+        return trips;
     }
     // stackless, parent links: state (node, the child slot the walk last came back from)
     long parent_walk(V3 o, V3 d, bool& hit_out) const
@@ -215,6 +283,16 @@ int main(int argc, char** argv)
     S.bvh4s = fb.bvh4s.data();
     S.bvh_tri4 = fb.bvh_tri4.data();
     Walker W(S, (int)fb.bvh4.size());
+    // the 4-wide node holding each leaf-order triangle k (the "hit leaf" of a ray leaving k)
+    std::vector<int> node_of_k(nt, -1);
+    for (int i = 0; i < (int)fb.bvh4.size(); i++)
+        for (const Bvh4Child& ch : fb.bvh4[i].ch)
+            if (ch.cnt > 0)
+                for (int j = 0; j < ch.cnt; j++) {
+                    int k;  // build_search_bvh stores the leaf-order index in the first record's w
+                    std::memcpy(&k, &fb.bvh_tri4[3 * (size_t)(ch.ref + j)].w, 4);
+                    if (k >= 0 && k < nt) node_of_k[k] = i;
+                }
 
     FILE* out = std::fopen(argv[2], "w");
     std::fprintf(out, "{\"what\": \"trips (dependent memory round trips) per occlusion walk over the product's search BVH, "
@@ -277,6 +355,71 @@ int main(int argc, char** argv)
             std::fprintf(out, ", \"%s\": {\"mean\": %.3f, \"p99\": %.0f, \"max\": %.0f}", names[w], mean,
                          v.empty() ? 0.0 : v[(size_t)(0.99 * (v.size() - 1))], v.empty() ? 0.0 : v.back());
             std::printf("%s %s mean %.2f p99 %.0f max %.0f\n", set ? "grazing" : "cosine", names[w], mean,
+                        v.empty() ? 0.0 : v[(size_t)(0.99 * (v.size() - 1))], v.empty() ? 0.0 : v.back());
+        }
+        std::fprintf(out, "}");
+    }
+    std::fprintf(out, "}, \"closest\": {");
+    // continuation walks from the hit leaf's ancestor: rays leaving a
+    // surface triangle; top-down from the root vs started at the ancestor `up` levels above
+    // the node holding the triangle, then the ancestors' other children
+    for (int set = 0; set < 2; set++) {
+        std::mt19937_64 rng(777 + set);
+        std::uniform_real_distribution<double> U(0.0, 1.0);
+        const int ups[4] = {0, 1, 2, 4};
+        std::vector<double> tr[5];
+        long mism = 0, used = 0;
+        for (int i = 0; i < n_rays / 4; i++) {
+            const int k0 = (int)(U(rng) * nt) % nt;  // original index
+            const int k = fb.prim2k[k0];
+            if (k < 0 || node_of_k[k] < 0) continue;
+            const float* t = &m.tris[9 * (size_t)k0];
+            double a[3], e1[3], e2[3], nrm[3];
+            for (int j = 0; j < 3; j++) a[j] = t[j], e1[j] = t[3 + j] - t[j], e2[j] = t[6 + j] - t[j];
+            nrm[0] = e1[1] * e2[2] - e1[2] * e2[1], nrm[1] = e1[2] * e2[0] - e1[0] * e2[2], nrm[2] = e1[0] * e2[1] - e1[1] * e2[0];
+            const double ln = std::sqrt(nrm[0] * nrm[0] + nrm[1] * nrm[1] + nrm[2] * nrm[2]);
+            if (!(ln > 0)) continue;
+            for (double& x : nrm) x /= ln;
+            double r1 = U(rng), r2 = U(rng);
+            if (r1 + r2 > 1) r1 = 1 - r1, r2 = 1 - r2;
+            double p[3];
+            for (int j = 0; j < 3; j++) p[j] = a[j] + r1 * e1[j] + r2 * e2[j] + 1e-4 * nrm[j];
+            double tx[3] = {1, 0, 0};
+            if (std::fabs(nrm[0]) > 0.9) tx[0] = 0, tx[1] = 1;
+            double ty[3] = {nrm[1] * tx[2] - nrm[2] * tx[1], nrm[2] * tx[0] - nrm[0] * tx[2], nrm[0] * tx[1] - nrm[1] * tx[0]};
+            const double lt = std::sqrt(ty[0] * ty[0] + ty[1] * ty[1] + ty[2] * ty[2]);
+            for (double& x : ty) x /= lt;
+            double tz[3] = {ty[1] * nrm[2] - ty[2] * nrm[1], ty[2] * nrm[0] - ty[0] * nrm[2], ty[0] * nrm[1] - ty[1] * nrm[0]};
+            const double phi = 2 * M_PI * U(rng);
+            const double ct = set == 0 ? std::sqrt(U(rng)) : 0.035 * U(rng);
+            const double sn = std::sqrt(std::max(0.0, 1 - ct * ct));
+            double dd[3];
+            for (int j = 0; j < 3; j++) dd[j] = ct * nrm[j] + sn * (std::cos(phi) * ty[j] + std::sin(phi) * tz[j]);
+            const V3 o = rtk::v3((float)p[0], (float)p[1], (float)p[2]);
+            const V3 d = rtk::normalize(rtk::v3((float)dd[0], (float)dd[1], (float)dd[2]));
+            float t0;
+            tr[0].push_back((double)W.closest_walk(o, d, 0, t0));
+            for (int u = 0; u < 4; u++) {
+                int st = node_of_k[k];
+                for (int l = 0; l < ups[u] && st != 0; l++) st = W.parent[st];
+                float t1;
+                tr[1 + u].push_back((double)W.closest_walk(o, d, st, t1));
+                mism += std::memcmp(&t1, &t0, 4) != 0;
+            }
+            used++;
+        }
+        const char* names[5] = {"root", "leaf_node", "up1", "up2", "up4"};
+        std::fprintf(out, "%s\"%s\": {\"rays\": %ld, \"answer_mismatches\": %ld", set ? ", " : "",
+                     set ? "grazing" : "cosine", used, mism);
+        for (int w = 0; w < 5; w++) {
+            std::vector<double> v = tr[w];
+            std::sort(v.begin(), v.end());
+            double sum = 0;
+            for (double x : v) sum += x;
+            const double mean = sum / std::max<size_t>(1, v.size());
+            std::fprintf(out, ", \"%s\": {\"mean\": %.3f, \"p99\": %.0f, \"max\": %.0f}", names[w], mean,
+                         v.empty() ? 0.0 : v[(size_t)(0.99 * (v.size() - 1))], v.empty() ? 0.0 : v.back());
+            std::printf("closest %s %s mean %.2f p99 %.0f max %.0f\n", set ? "grazing" : "cosine", names[w], mean,
                         v.empty() ? 0.0 : v[(size_t)(0.99 * (v.size() - 1))], v.empty() ? 0.0 : v.back());
         }
         std::fprintf(out, "}");
