@@ -223,6 +223,16 @@ int upload(rt_context* c, DevBuf& b, const std::vector<T>& v)
 
 
 // ------------------------------------------------------------ wave helpers
+#ifndef RT_DEBUG_FB
+#define RT_DEBUG_FB 0  // study builds: count k_trace's exact-walk hand-overs and the octet walks'
+                       // parks of the timed renders, printed on stderr after each run_wave
+#endif
+#if RT_DEBUG_FB
+__device__ unsigned long long rt_dbg_fb[8];  // k_trace closest fallbacks, octet parks, occlusion fallbacks, overflows, ties, chain fails, from rows, -
+#define RT_DBG(i) atomicAdd(&rt_dbg_fb[i], 1ull)
+#else
+#define RT_DBG(i) ((void)0)
+#endif
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
 
 // Wave-aggregated append: every lane of the wave must call this converged.
@@ -580,6 +590,7 @@ __device__ void exact_octets(const rtk::WaveView& W, int par, uint32_t* lds, int
             } else if (T.steps >= W.budget && (ANY ? rtk::octa_parkable(T) : rtk::octc_parkable(T))) {
                 int ps = 0;
                 if (sub == 0) ps = atomicAdd(parked, 1);
+                if (sub == 0) RT_DBG(1);
                 ps = __shfl(ps, rtk::oct_lane0());
                 if (ps < W.park_cap) {
                     if (ANY)
@@ -859,6 +870,20 @@ struct RowInQuadStack {
     __device__ __forceinline__ void set_rec(int i, uint32_t rv) { r[(i >> 2) * 64 + (i & 3)] = rv; }
 };
 
+#if RT_DRAIN_STRONG_FENCE  // (study build: the hand-off's ordering made explicit)
+#define RT_DRAIN_FENCE()                                       \
+    do {                                                       \
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup"); \
+        __builtin_amdgcn_s_waitcnt(0);                         \
+        __builtin_amdgcn_wave_barrier();                       \
+    } while (0)
+#else
+#define RT_DRAIN_FENCE()                                       \
+    do {                                                       \
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront"); \
+        __builtin_amdgcn_wave_barrier();                       \
+    } while (0)
+#endif
 #ifndef RT_DRAIN_ROWS
 #define RT_DRAIN_ROWS 3  // k_trace: once a wave's stream is out and at most this many quads still walk,
                          // their walks continue as rows (rt_row.h); 0 = off. cfg4 8-way shard, one
@@ -919,6 +944,9 @@ __device__ __forceinline__ void trace_stream(const rtk::WaveView& W, const RtSce
             } else {  // the exact walk answers it (k_step(i)); the queue record again (o.w: slot)
                 fbl[atomicAdd(fbn, 1)] = rtk::RayRec{rtk::f4(q.o, rt_asfloat(target >> 3)),
                                                      rtk::f4(q.d, rt_asfloat(target & 7u))};
+                RT_DBG(ANY ? 2 : 0);
+                RT_DBG(why == 3 ? 3 : why == 1 ? 4 : 5);
+                if (gs == 16) RT_DBG(6);
                 atomicAdd(&W.r_park[target >> 3], 1);
                 if (STATS && W.iterq && W.iter < RT_MAX_TIMED_ITERS)
                     atomicAdd(W.iterq + 2 * RT_MAX_TIMED_ITERS + 4 * W.iter + 3, 1);  // (RT_ITER_LOG: fallbacks)
@@ -1008,13 +1036,11 @@ __device__ __forceinline__ void trace_stream(const rtk::WaveView& W, const RtSce
         float k0 = 0.0f, k1 = 0.0f;
         if (ract && sub < q.sp) r0 = qr[sub * 64 + sq], k0 = qk[sub * 64 + sq];
         if (ract && sub + 16 < q.sp) r1 = qr[(sub + 16) * 64 + sq], k1 = qk[(sub + 16) * 64 + sq];
-        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-        __builtin_amdgcn_wave_barrier();
+        RT_DRAIN_FENCE();
         RowInQuadStack rs{qr + 4 * row, qk + 4 * row};
         if (ract && sub < q.sp) rs.set(sub, r0, k0);
         if (ract && sub + 16 < q.sp) rs.set(sub + 16, r1, k1);
-        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-        __builtin_amdgcn_wave_barrier();
+        RT_DRAIN_FENCE();
         active = ract;
         while (__any(active)) {
             if (STATS) {
@@ -2404,6 +2430,20 @@ int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounces, cons
             }
         }
     }
+#if RT_DEBUG_FB
+    {
+        unsigned long long v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        HIPCHK(c, hipStreamSynchronize(s));
+        for (int l = 0; l < nl; l++) HIPCHK(c, hipStreamSynchronize(L[l].s));
+        HIPCHK(c, hipMemcpyFromSymbol(v, HIP_SYMBOL(rt_dbg_fb), sizeof v));
+        int its = 0;
+        for (int l = 0; l < nl; l++) its = std::max(its, L[l].it);
+        fprintf(stderr, "[rt dbg] n=%d iters=%d k_trace fallbacks closest=%llu any=%llu (overflow %llu tie %llu chain %llu; rows %llu) octet parks=%llu closest row drains=%llu\n",
+                n, its, v[0], v[2], v[3], v[4], v[5], v[6], v[1], v[7]);
+        const unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        HIPCHK(c, hipMemcpyToSymbol(HIP_SYMBOL(rt_dbg_fb), z, sizeof z));
+    }
+#endif
     return RT_OK;
 }
 
