@@ -600,7 +600,7 @@ def main():
             stats_seq = rk.stats()
         rk.set_stats(False)
 
-    elapsed, full, kernel_ms = None, None, None
+    elapsed, full, kernel_ms, handovers = None, None, None, None
     if not args.roofline_only:
         for _ in range(args.warmup):
             frame.render(stream)
@@ -608,6 +608,7 @@ def main():
                 frame.gather()
         torch.cuda.synchronize(dev)
 
+        rk.exact_handovers(reset=True)  # (waits for the device: before the timed region)
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize(dev)
@@ -627,6 +628,7 @@ def main():
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
         kernel_ms = float(np.mean(kms))
+        handovers = rk.exact_handovers()  # (this rank's devices, the timed renders)
 
     # roofline pass: one lane (one stream), HIP events around every launch
     ktime, lane1_ms = None, None
@@ -773,6 +775,12 @@ def main():
             "cpu_baseline": cpu,
             "parity": parity,
         }
+        if handovers is not None:
+            # the search-BVH walks' health: queries the timed renders handed to the exact octree
+            # walk (ties, failed verifications, overflows), rank 0's devices; ~2e-6 per sample
+            ms = samples_rank * args.steps / 1e6
+            out["exact_handovers"] = {"per_frame": round(handovers / args.steps, 1),
+                                      "per_msample": round(handovers / ms, 3) if ms > 0 else None}
         if strong is not None:
             out["strong_cfg4"] = strong
             # the north star's fixed-size figure beside the weak-scaling value: cfg4 (its 8-GPU

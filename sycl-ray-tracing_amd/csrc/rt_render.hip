@@ -162,6 +162,7 @@ struct Backend {
     DevBuf nodes, tri4, prim2k, mat_idx, mats, emissive, spheres, env, env_lum, cdf;
     DevBuf bvh4, bvh16, bvh4s, bvh16s, bvh_tri4, parent, leaf_of, cdf_row, cdf_coarse, cdf_fence, matk;
     DevBuf stats;     // 2 x RT_STAT_COUNT u64: all kernels, then the tail kernel's share
+    DevBuf handovers; // u64: queries k_trace handed to the exact walk, every render since the last reset
     DevBuf iterq;     // stats renders: per-iteration {queries, live slots} (RT_ITER_LOG)
     DevBuf wlog;      // stats renders with a walk log: count (256 B), then 3 float4 per record
     DevBuf wave[RT_MAX_LANES];      // per lane: path state, pending records, results, queues, lists
@@ -743,6 +744,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_STEP_OCC
     if (blockIdx.x == 0 && threadIdx.x == 0) {  // for k_trace(i + 1); DONE[par ^ 1] was released by k_trace(i)
         cnt[C_FBC0 + (par ^ 1)] = cnt[C_FBA0 + (par ^ 1)] = 0;
         cnt[C_DONE0 + (par ^ 1)] = 0;
+        // (k_trace(i)'s hand-overs to the exact walk, summed for rt_device_exact_handovers: a
+        // health figure, ~1e-6 of the queries; a search-BVH walk that went wrong shows here)
+        const int nf = cnt[C_FBC0 + par] + cnt[C_FBA0 + par];
+        if (W.handovers && nf > 0) atomicAdd(W.handovers, (unsigned long long)nf);
     }
     rtk::Stats st;
     if (STATS)
@@ -1927,6 +1932,10 @@ int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounces, cons
         if (int r = ensure(c, b->wlog, 256 + (size_t)dg.wlog_cap * 48)) return r;
         HIPCHK(c, hipMemsetAsync(b->wlog.p, 0, 256, s));
     }
+    if (!b->handovers.p) {
+        if (int r = ensure(c, b->handovers, 8)) return r;
+        HIPCHK(c, hipMemsetAsync(b->handovers.p, 0, 8, s));
+    }
     if (S && iter_log) {
         if (int r = ensure(c, b->iterq, RT_MAX_TIMED_ITERS * 24)) return r;
         HIPCHK(c, hipMemsetAsync(b->iterq.p, 0, RT_MAX_TIMED_ITERS * 24, s));
@@ -2059,6 +2068,7 @@ int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounces, cons
             HIPCHK(c, hipMemsetAsync(b->fcnt[l].p, 0, C_COUNT * sizeof(int32_t), La.s));
         }
         W.iterq = (S && iter_log && l == 0) ? (int32_t*)b->iterq.p : nullptr;
+        W.handovers = (unsigned long long*)b->handovers.p;
         if (wlog) {
             W.wlog_n = (int32_t*)b->wlog.p;
             W.wlog = (float4_*)((char*)b->wlog.p + 256);
@@ -2842,6 +2852,27 @@ extern "C" double rt_device_last_kernel_ms(rt_context* c)
 
 // Iterations the last wavefront render took.
 extern "C" int rt_device_last_iterations(rt_context* c) { return c && c->backend ? be(c)->last_iters : -1; }
+
+// Queries k_trace handed to the exact octree walk (ties, failed verifications, stack
+// overflows, far origins, the force_fallback stressor) in every render on every device of
+// the context since the last reset: the walks' health figure (~2e-6 per sample on cfg2).
+// Waits for the devices.
+extern "C" int rt_device_exact_handovers(rt_context* c, unsigned long long* out, int reset)
+{
+    if (!c || !c->backend || !out) return RT_ERR_ARG;
+    unsigned long long sum = 0;
+    for (Backend* b : grp(c)->dev) {
+        HIPCHK(c, hipSetDevice(b->device));
+        HIPCHK(c, hipDeviceSynchronize());
+        if (!b->handovers.p) continue;
+        unsigned long long v = 0;
+        HIPCHK(c, hipMemcpy(&v, b->handovers.p, 8, hipMemcpyDeviceToHost));
+        sum += v;
+        if (reset) HIPCHK(c, hipMemset(b->handovers.p, 0, 8));
+    }
+    *out = sum;
+    return RT_OK;
+}
 
 // Per-kernel-class timing (k_trace, k_step, k_tail) over the renders since it
 // was enabled, summed over the context's devices: out_ms[3] total ms (HIP events

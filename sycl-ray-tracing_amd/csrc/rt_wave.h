@@ -122,6 +122,7 @@ struct WaveView {
     float* fspill_k;
     int fspill_lanes;
     int32_t* iterq;         // stats renders: [iteration][2] = {queries, live slots} (else null)
+    unsigned long long* handovers;  // queries k_trace handed to the exact walk, summed over renders (device; else null)
     float4_* wlog;          // stats renders with a walk log (rt_test_walk_log): 3 float4 per long walk, else null
     int32_t* wlog_n;        // records written (may exceed wlog_cap: the rest are dropped)
     int wlog_min, wlog_cap; // quad_visit calls a logged walk takes at least; records at most

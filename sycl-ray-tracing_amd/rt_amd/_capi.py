@@ -84,6 +84,7 @@ _SIGS = {
     "rt_device_kernel_timing": (I, [P, I, P, P]),
     "rt_device_set_lanes": (I, [P, I]),
     "rt_device_last_iterations": (I, [P]),
+    "rt_device_exact_handovers": (I, [P, P, I]),
     "rt_device_queries": (I, [P, I, P, I, I, P, P, P]),
     # hostsim-only extra
     "rt_hostsim_heap_order": (I, [P, I, P, P]),

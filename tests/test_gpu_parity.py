@@ -369,6 +369,29 @@ def test_gpu_parked_walks_small_launches(name, budget, every, tail, manifest, ca
     assert_parity(got, e["expected"], min_bitwise=1.0)
 
 
+def test_gpu_exact_handovers_are_rare(manifest, cameras):
+    """The search-BVH walks' health in the product's timed kernels (not the stats variant):
+    queries k_trace hands to the exact octree walk (rt_device_exact_handovers) stay at the
+    ~1e-6-per-sample level of ties on the dragon (a walk that went wrong, e.g. a corrupted
+    stack, still renders the reference's image through the exact walk, only slower: this is
+    where it shows), and the counter does count: the force_fallback stressor raises it."""
+    e = rt_cases.golden_case("cfg2_dragon", manifest)
+    rk, fb = rt_cases.make_kernel(e, cameras, hostsim=False, W=480, H=270, spp=8)
+    samples = 480 * 270 * 8
+    rk.render()
+    rk.exact_handovers(reset=True)
+    rk.render()
+    ho = rk.exact_handovers()
+    print("hand-overs", ho, "per sample", ho / samples)
+    assert ho <= 1e-4 * samples
+    rk.test_schedule(force_fallback=64)
+    rk.exact_handovers(reset=True)
+    rk.render()
+    forced = rk.exact_handovers(reset=True)
+    print("forced hand-overs", forced)
+    assert forced > 0.01 * samples
+
+
 @pytest.mark.parametrize("name,off,stride", [("cfg3_dragon", 311, 400), ("cfg4_dragon4k", 1083, 1100)])
 def test_gpu_full_rows_at_256spp_match_oracle(name, off, stride, manifest, cameras):
     """Cfg3 (1080p) and Cfg4 (4K) at their full 256 spp: whole image rows
