@@ -1047,6 +1047,19 @@ __device__ __forceinline__ void trace_stream(const rtk::WaveView& W, const RtSce
         if (ract && sub + 16 < q.sp) rs.set(sub + 16, r1, k1);
         RT_DRAIN_FENCE();
         active = ract;
+#if RT_DRAIN_RESTART == 1  // (study build: the row walk restarts at the root, the quad's stack dropped)
+        q.sp = 0;
+        if (q.cur != 0x7fffffff) q.cur = 0;
+#elif RT_DRAIN_RESTART == 2  // (study build: a new walk of the same ray, nothing of the quad's kept)
+        if (ract) rtk::qstate_begin<ANY>(q, q.o, q.d, sub, nullptr);
+#elif RT_DRAIN_RESTART == 3  // (study build: the ray's box-test form recomputed from o and d)
+        q.rb = rtk::rayb_setup(q.o, q.d);
+#elif RT_DRAIN_RESTART == 4  // (study build: the walk's hit record reset; the walk goes on from its stack)
+        q.h.t = __builtin_inff(), q.h.t2 = __builtin_inff(), q.h.k = ANY ? 0 : -1, q.h.leaf = -1;
+        q.h.prim = 0x7fffffff, q.h.tie = false, q.h.ovf = false;
+        q.sp = 0;
+        if (q.cur != 0x7fffffff) q.cur = 0;
+#endif
         while (__any(active)) {
             if (STATS) {
                 if (active && sub == 0) ps->c[RT_STAT_DRAIN_VISITS]++;
