@@ -54,6 +54,9 @@ namespace {
 #define RT_FAST_SPP 2.25      // ... from iteration RT_FAST_SPP x spp on
 #define RT_FAST_MAX_SPP 4096  // ... in renders of at most this many samples per pixel
 #define RT_LANES4_MAX 1572864  // auto lanes: 4 at most this many slots per launch, else 3
+#ifndef RT_STEP_FILL
+#define RT_STEP_FILL 8  // k_step: blocks per CU at most (one slot per thread below that; waves stride over chunks above)
+#endif
 #ifndef RT_STEP_OCC
 #define RT_STEP_OCC 3  // k_step waves per SIMD
 #endif
@@ -2113,7 +2116,7 @@ int run_wave(rt_context* c, Backend* b, int w, int h, int spp, int bounces, cons
     // (k_step: at least 3 blocks, one per exact-walk role and one for the path step, so a
     // small live count with fallbacks or parked walks pending still steps its paths)
     auto step_blocks_of = [&](const WaveLane& La) {
-        return (int)std::max(3l, std::min((La.live + threads - 1) / threads, (long)dev_cus * 8));
+        return (int)std::max(3l, std::min((La.live + threads - 1) / threads, (long)dev_cus * RT_STEP_FILL));
     };
     auto trace_blocks_of = [&](const WaveLane& La) {
         const long want = (20 * La.live + 2 * threads - 1) / (2 * threads);
