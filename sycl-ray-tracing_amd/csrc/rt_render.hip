@@ -1022,7 +1022,10 @@ __device__ __forceinline__ void trace_stream(const rtk::WaveView& W, const RtSce
         const int row = lane >> 4;
         unsigned long long m = bact;
         for (int i = 0; i < row; i++) m &= m - 1ull;
-        const int src = m ? __ffsll((long long)m) - 1 : 0;  // the walking quad's lane 0
+#ifndef RT_DRAIN_SRC_LANE
+#define RT_DRAIN_SRC_LANE 0  // (study: which lane of the walking quad hands its state to the row)
+#endif
+        const int src = (m ? __ffsll((long long)m) - 1 : 0) + RT_DRAIN_SRC_LANE;  // the walking quad's lane
         const bool ract = m != 0;
         // its state (quad-uniform) to the row's lanes
         auto pf = [&](float v) { return __shfl(v, src); };
