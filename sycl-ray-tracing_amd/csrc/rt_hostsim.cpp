@@ -52,7 +52,8 @@ struct OmpShare {
 
 // The product's wavefront loop (rt_render.hip run_wave) on the host:
 // same stage functions, same queues; appends are plain atomics.
-static void host_append(const rtk::WaveView& W, int32_t* act_count, int p, const rtk::Emit& e)
+template <class E>
+static void host_append(const rtk::WaveView& W, int32_t* act_count, int p, const E& e)
 {
     for (int k = 0; k < rtk::RK_COUNT; k++)
         if ((e.mask >> k) & 1u) W.q[k][__atomic_fetch_add(&W.counters[k], 1, __ATOMIC_RELAXED)] = e.rec(k, p);
@@ -242,7 +243,10 @@ static int run_wave_host(rt_context* c, int w, int h, int spp, int bounces, cons
 #pragma omp for schedule(dynamic, 64)
             for (int idx = 0; idx < n_in; idx++) {
                 const int p = W.act_in[idx];
-                rtk::Emit e;
+                // (the step's rays in a column, as k_step keeps them in LDS: rt_wave.h EmitLds)
+                float col[6 * rtk::RK_COUNT];
+                rtk::EmitLds<1> e;
+                e.s = col;
                 rtk::path_step(W, p, e, ps);
                 host_append(W, &act[par ^ 1], p, e);
             }
