@@ -54,11 +54,15 @@ namespace {
 #define RT_FAST_SPP 2.25      // ... from iteration RT_FAST_SPP x spp on
 #define RT_FAST_MAX_SPP 4096  // ... in renders of at most this many samples per pixel
 #define RT_LANES4_MAX 1572864  // auto lanes: 4 at most this many slots per launch, else 3
-#ifndef RT_STEP_FILL
-#define RT_STEP_FILL 8  // k_step: blocks per CU at most (one slot per thread below that; waves stride over chunks above)
-#endif
 #ifndef RT_STEP_OCC
 #define RT_STEP_OCC 3  // k_step waves per SIMD
+#endif
+#ifndef RT_STEP_FILL
+// k_step: blocks per CU at most, one grid-fill at its occupancy (one slot per thread below
+// that; above, each wave strides over 64-slot chunks). cfg2 over 4 A/B rounds on 2 boxes:
+// 8 / 4 / 3 / 2 -> 128.8-129.3 / 128.5-128.9 / 128.0-128.4 / 127.3-128.4 ms
+// (profiles/r06_step_fill_ab.json)
+#define RT_STEP_FILL RT_STEP_OCC
 #endif
 #ifndef RT_TAIL_ROWS
 #define RT_TAIL_ROWS 1  // k_tail walks with rows (rt_row.h)
