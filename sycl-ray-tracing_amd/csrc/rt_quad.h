@@ -261,6 +261,9 @@ __device__ __forceinline__ bool qstate_begin(QState& q, V3 o, V3 d, int sub, Sta
 // more exact-walk fallbacks) were slower (profiles/r02_k_trace_variants.jsonl).
 // PAIR = false (stats renders only, rt_set_stats(ctx, 2)): occlusion walks take one node per
 // trip, so their box-test counters are the necessary ones (answers do not depend on the order).
+#ifndef RT_POP_PAIRED
+#define RT_POP_PAIRED 1
+#endif
 template <bool ANY, int DESC = RT_VISIT_DESCEND, bool PAIR = true, class QSTK>
 __device__ __forceinline__ int quad_visit(const RtSceneView& S, QState& q, QSTK& stk, int sub, Stats* st)
 {
@@ -440,11 +443,40 @@ __device__ __forceinline__ int quad_visit(const RtSceneView& S, QState& q, QSTK&
     const float tmax = h.t + h.t * RT_T2_WINDOW;
     int nxt = 0x7fffffff;
     while (q.sp > 0) {
+#if RT_POP_PAIRED >= 2  // two entries per LDS round trip: the pops past a closed window run in pairs
+        if (q.sp >= 2) {
+            const float k1 = stk.key(q.sp - 1), k2 = stk.key(q.sp - 2);
+            const int r1 = (int)stk.rec(q.sp - 1), r2 = (int)stk.rec(q.sp - 2);
+            rt_pin(r1);
+            rt_pin(r2);
+            if (k1 <= tmax) {
+                q.sp -= 1;
+                nxt = r1;
+                break;
+            }
+            q.sp -= 2;
+            if (k2 <= tmax) {
+                nxt = r2;
+                break;
+            }
+            continue;
+        }
+#endif
         --q.sp;
+#if RT_POP_PAIRED  // the entry's key and item read together: one LDS round trip per pop, not two
+        const float kk = stk.key(q.sp);
+        const int rr = (int)stk.rec(q.sp);
+        rt_pin(rr);  // (else the compiler sinks the item's read past the loop: two round trips)
+        if (kk <= tmax) {
+            nxt = rr;
+            break;
+        }
+#else
         if (stk.key(q.sp) <= tmax) {
             nxt = (int)stk.rec(q.sp);
             break;
         }
+#endif
     }
     q.cur = nxt;
     return nxt == 0x7fffffff ? 1 : 0;

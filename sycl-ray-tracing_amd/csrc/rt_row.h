@@ -155,7 +155,13 @@ __device__ __forceinline__ int row_visit(const RtSceneView& S, QState& q, RSTK& 
         for (int g = 1; g < 4; g++) {
             if (nl != g || q.sp == 0) break;
             const int t = (int)stk.rec(q.sp - 1);
+#if RT_POP_PAIRED
+            const float tk = ANY ? 0.0f : stk.key(q.sp - 1);  // (read with the item: one LDS round trip)
+            if (!ANY) rt_pin(tk);
+            if (t >= 0 || (!ANY && !(tk <= tw))) break;  // an inner node, or closed by the window
+#else
             if (t >= 0 || (!ANY && !(stk.key(q.sp - 1) <= tw))) break;  // an inner node, or closed by the window
+#endif
             q.sp--;
             nl++;
             (g == 1 ? l1 : g == 2 ? l2 : l3) = t;
@@ -228,11 +234,40 @@ __device__ __forceinline__ int row_visit(const RtSceneView& S, QState& q, RSTK& 
     const float tmax = h.t + h.t * RT_T2_WINDOW;
     int nxt = 0x7fffffff;
     while (q.sp > 0) {
+#if RT_POP_PAIRED >= 2  // two entries per LDS round trip: the pops past a closed window run in pairs
+        if (q.sp >= 2) {
+            const float k1 = stk.key(q.sp - 1), k2 = stk.key(q.sp - 2);
+            const int r1 = (int)stk.rec(q.sp - 1), r2 = (int)stk.rec(q.sp - 2);
+            rt_pin(r1);
+            rt_pin(r2);
+            if (k1 <= tmax) {
+                q.sp -= 1;
+                nxt = r1;
+                break;
+            }
+            q.sp -= 2;
+            if (k2 <= tmax) {
+                nxt = r2;
+                break;
+            }
+            continue;
+        }
+#endif
         --q.sp;
+#if RT_POP_PAIRED  // the entry's key and item read together: one LDS round trip per pop, not two
+        const float kk = stk.key(q.sp);
+        const int rr = (int)stk.rec(q.sp);
+        rt_pin(rr);  // (else the compiler sinks the item's read past the loop: two round trips)
+        if (kk <= tmax) {
+            nxt = rr;
+            break;
+        }
+#else
         if (stk.key(q.sp) <= tmax) {
             nxt = (int)stk.rec(q.sp);
             break;
         }
+#endif
     }
     q.cur = nxt;
     return nxt == 0x7fffffff ? 1 : 0;
