@@ -405,10 +405,41 @@ __device__ __forceinline__ int shard_find(const int* pre, int m, int g)
     return lo;
 }
 
+// The same search with M (a compile-time table size) as an 8-way search: each round reads 7
+// entries at once (independent LDS reads, one round trip) and advances by the count at or below
+// g (the table is non-decreasing), so 448 entries take 3 dependent round trips instead of 9 and
+// 64 take 2 instead of 6. k_trace's refill (on ~4 of 5 wave trips, the whole wave waiting) and
+// every k_step / k_tail chunk start search these tables.
+#ifndef RT_FIND8
+#define RT_FIND8 1
+#endif
+template <int M>
+__device__ __forceinline__ int shard_find8(const int* pre, int g)
+{
+#if RT_FIND8
+    constexpr int TOP = M > 512 ? 512 : M > 64 ? 64 : M > 8 ? 8 : 1;
+    static_assert(M <= 4096, "three or four 8-way rounds");
+    int lo = 0;
+#pragma unroll
+    for (int step = TOP; step >= 1; step >>= 3) {
+        int c = 0;
+#pragma unroll
+        for (int k = 1; k < 8; k++) {
+            const int j = lo + step * k;
+            c += (j < M && pre[j] <= g) ? 1 : 0;
+        }
+        lo += step * c;
+    }
+    return lo;
+#else
+    return shard_find(pre, M, g);
+#endif
+}
+
 // Queue item of stream position g (segment table pre[0..RT_NSEG], k_trace): the ray and its kind.
 __device__ __forceinline__ rtk::RayRec queue_item_at(const rtk::WaveView& W, const int* pre, int g, int& kind)
 {
-    const int j = shard_find(pre, RT_NSEG, g);
+    const int j = shard_find8<RT_NSEG>(pre, g);
     const SegId s = seg_id(j);
     kind = s.kind;
     // (the queue base by selects: W.q[kind] with a lane-varying kind would be a load)
@@ -808,7 +839,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_STEP_OCC
         e.heavy = false;
         int p = -1;
         if (idx < n) {
-            const int sh = shard_find(s_pre, RT_QSHARDS, idx);
+            const int sh = shard_find8<RT_QSHARDS>(s_pre, idx);
             p = W.act_in[(size_t)sh * W.seg_cap + (idx - s_pre[sh])];
             rtk::path_step(W, p, e, ps);
         }
@@ -827,7 +858,7 @@ __global__ __launch_bounds__(256) void k_hand(rtk::WaveView W, int par)
     shard_prefix(W.counters, RT_QSHARDS, [&](int j) { return ac_at(par, j); }, s_pre);
     const int n = s_pre[RT_QSHARDS];
     for (int idx = (int)(blockIdx.x * blockDim.x + threadIdx.x); idx < n; idx += (int)(gridDim.x * blockDim.x)) {
-        const int sh = shard_find(s_pre, RT_QSHARDS, idx);
+        const int sh = shard_find8<RT_QSHARDS>(s_pre, idx);
         const int p = W.act_in[(size_t)sh * W.seg_cap + (idx - s_pre[sh])];
         if ((int)rt_asuint(W.p_thr[p].w) > W.fast_thr || W.r_park[p] != 0) continue;
         const int j = atomicAdd(W.fast_ticket, 1);
@@ -844,7 +875,7 @@ __global__ __launch_bounds__(256) void k_hist(rtk::WaveView W, int par, int32_t*
     shard_prefix(W.counters, RT_QSHARDS, [&](int j) { return ac_at(par, j); }, s_pre);
     const int n = s_pre[RT_QSHARDS];
     for (int idx = (int)(blockIdx.x * blockDim.x + threadIdx.x); idx < n; idx += (int)(gridDim.x * blockDim.x)) {
-        const int sh = shard_find(s_pre, RT_QSHARDS, idx);
+        const int sh = shard_find8<RT_QSHARDS>(s_pre, idx);
         const int p = W.act_in[(size_t)sh * W.seg_cap + (idx - s_pre[sh])];
         atomicAdd(hist + min((int)rt_asuint(W.p_thr[p].w), W.spp), 1);
     }
@@ -1323,7 +1354,7 @@ __device__ __forceinline__ void tail_body(const rtk::WaveView& W, int par, unsig
             if (base + nneed >= n) drained = true;
             const int idx = base + __popcll(bneed & ((1ull << lane) - 1ull));
             if (need && idx < n) {
-                const int sh = shard_find(s_pre, RT_QSHARDS, idx);
+                const int sh = shard_find8<RT_QSHARDS>(s_pre, idx);
                 my = W.act_in[(size_t)sh * W.seg_cap + (idx - s_pre[sh])];
                 if (FAST) W.r_park[my] = 0;  // (k_hand's mark)
             }
