@@ -436,18 +436,52 @@ __device__ __forceinline__ int shard_find8(const int* pre, int g)
 #endif
 }
 
-// Queue item of stream position g (segment table pre[0..RT_NSEG], k_trace): the ray and its kind.
-__device__ __forceinline__ rtk::RayRec queue_item_at(const rtk::WaveView& W, const int* pre, int g, int& kind)
+// Where stream position g's queue record lives (segment table pre[0..RT_NSEG]) and its kind.
+__device__ __forceinline__ const rtk::RayRec* queue_item_ptr(const rtk::WaveView& W, const int* pre, int g, int& kind)
 {
     const int j = shard_find8<RT_NSEG>(pre, g);
     const SegId s = seg_id(j);
     kind = s.kind;
-    // (the queue base by selects: W.q[kind] with a lane-varying kind would be a load)
     rtk::RayRec* qk = W.q[0];
 #pragma unroll
     for (int k2 = 1; k2 < rtk::RK_COUNT; k2++) qk = s.kind == k2 ? W.q[k2] : qk;
-    // (heavy shard h: after the kind's RT_QSHARDS segments, RT_QSHARDS / RT_HSHARDS seg_caps each)
-    return qk[qbase(s.heavy, s.shard, W.seg_cap) + (g - pre[j])];
+    return qk + qbase(s.heavy, s.shard, W.seg_cap) + (g - pre[j]);
+}
+
+// Queue item of stream position g (segment table pre[0..RT_NSEG], k_trace): the ray and its kind.
+__device__ __forceinline__ rtk::RayRec queue_item_at(const rtk::WaveView& W, const int* pre, int g, int& kind)
+{
+    // (the queue base by selects: W.q[kind] with a lane-varying kind would be a load; heavy
+    // shard h: after the kind's RT_QSHARDS segments, RT_QSHARDS / RT_HSHARDS seg_caps each)
+    return *queue_item_ptr(W, pre, g, kind);
+}
+
+// k_trace's look-ahead (RT_TRACE_PREFETCH): right after a refill, the wave's next 16 stream
+// positions are copied into its LDS buffer by direct-to-LDS loads (lane 2i + h: half h of
+// record i, 16 B; the hardware puts lane L's 16 B at buf + 16 L), their kinds alongside; the next
+// refill takes its records from there (a refill needs at most 16 positions, all from the
+// cursor on, which the buffer starts at), so the refill no longer waits on the queue's memory.
+#ifndef RT_TRACE_PREFETCH
+#define RT_TRACE_PREFETCH 1
+#endif
+struct QPrefetch {
+    float4_* buf;  // the wave's 64 x 16 B (records 0..15 in the first 512 B)
+    int* kind;     // the wave's 16 kinds (-1: past the end of the stream)
+};
+__device__ __forceinline__ void queue_prefetch(const rtk::WaveView& W, const int* pre, const QPrefetch& pf, int first, int cursor,
+                                               int wg, int wn, int total)
+{
+    const int lane = lane_id(), i = lane >> 1;
+    const int j = cursor + i;
+    const int idx = (wg + (j >> 4) * wn) * 16 + (j & 15);
+    const bool ok = lane < 32 && idx < total;
+    int kind = -1;
+    if (ok) {
+        const rtk::RayRec* rp = queue_item_ptr(W, pre, first + idx, kind);
+        __builtin_amdgcn_global_load_lds((const void*)((const float4_*)rp + (lane & 1)),
+                                         (__attribute__((address_space(3))) void*)pf.buf, 16, 0, 0);
+    }
+    if (lane < 32 && (lane & 1) == 0) pf.kind[i] = ok ? kind : -1;
 }
 
 // Path init: every slot seeds its RNG and emits its first camera ray (into Q[0], ACT[0]).
@@ -943,7 +977,7 @@ struct RowInQuadStack {
 template <bool ANY, bool STATS, bool PAIR, int G, class QSTK>
 __device__ __forceinline__ void trace_stream(const rtk::WaveView& W, const RtSceneView& S, QSTK& stk, const int* s_pre,
                                              int first, int total, int wg, int wn, int32_t* fbn, rtk::RayRec* fbl,
-                                             rtk::Stats* ps)
+                                             rtk::Stats* ps, const QPrefetch& pf)
 {
     static_assert(G == 4 || G == 16, "quads or rows");
     constexpr unsigned long long ALL_IDLE = G == 4 ? 0x1111111111111111ull : 0x0001000100010001ull;
@@ -955,6 +989,9 @@ __device__ __forceinline__ void trace_stream(const rtk::WaveView& W, const RtSce
     bool active = false;
     uint32_t target = 0;
     rtk::QState q;  // (its ray is the query's: a fallback record is rebuilt from q.o, q.d and target)
+#if RT_TRACE_PREFETCH
+    if (!exhausted) queue_prefetch(W, s_pre, pf, first, cursor, wg, wn, total);
+#endif
     // a walk's end: its answer, or the exact walk's list; gs = lanes of the group walking it
     auto finish = [&](int res, int gs) {
         // a long walk: the path's next rays go to the heavy class (head of the next streams)
@@ -1003,8 +1040,19 @@ __device__ __forceinline__ void trace_stream(const rtk::WaveView& W, const RtSce
                 const int j = cursor + __popcll(bidle & ((1ull << (qd * G)) - 1ull));  // this group's stream position
                 const int idx = (wg + (j >> 4) * wn) * 16 + (j & 15);
                 if (idx < total) {
+#if RT_TRACE_PREFETCH
+                    const int slot = j - cursor;  // (0..15: the buffer starts at the cursor)
+                    // (the compiler does not order LDS reads after direct-to-LDS loads: wait for
+                    // the vector-memory counter here, vmcnt(0), before reading the buffer)
+                    __builtin_amdgcn_s_waitcnt(0x0F70);
+                    rtk::RayRec r;
+                    r.o = pf.buf[2 * slot];
+                    r.d = pf.buf[2 * slot + 1];
+                    const int kind = pf.kind[slot];
+#else
                     int kind;
                     rtk::RayRec r = queue_item_at(W, s_pre, first + idx, kind);
+#endif
                     target = (rt_asuint(r.o.w) << 3) | (uint32_t)kind;
                     if (forced_fallback(W, r.o, r.d)) {
                         if (sub == 0) {
@@ -1025,6 +1073,12 @@ __device__ __forceinline__ void trace_stream(const rtk::WaveView& W, const RtSce
             }
             cursor += __popcll(bidle);
             exhausted = (wg + (cursor >> 4) * wn) * 16 >= total;
+#if RT_TRACE_PREFETCH
+            // (every lane has read its record: the buffer is free for the next 16 positions)
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            if (!exhausted) queue_prefetch(W, s_pre, pf, first, cursor, wg, wn, total);
+#endif
             if (STATS && lane == 0) ps->c[RT_STAT_REFILLS]++;
         }
         const unsigned long long bact = __ballot(active && sub == 0);
@@ -1123,6 +1177,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_OC
 {
     __shared__ uint32_t s_lds[RT_LDS_WORDS * 256];
     __shared__ int s_pre[RT_NSEG + 1];
+    __shared__ float4_ s_qbuf[RT_TRACE_PREFETCH ? 4 : 1][64];  // per wave: the next 16 stream records (queue_prefetch)
+    __shared__ int s_qkind[RT_TRACE_PREFETCH ? 4 : 1][16];
+    const QPrefetch pf{s_qbuf[RT_TRACE_PREFETCH ? threadIdx.x >> 6 : 0], s_qkind[RT_TRACE_PREFETCH ? threadIdx.x >> 6 : 0]};
     int32_t* cnt = W.counters;
     if (blockIdx.x == 0) {  // filled by k_step(i) next
         for (int j = threadIdx.x; j < (rtk::RK_COUNT + 1) * RT_QSHARDS; j += blockDim.x)
@@ -1173,16 +1230,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_TRACE_OC
     if constexpr (G == 4) {
         rtk::QuadStack<RT_QSTACK, 64> stk{s_lds + (threadIdx.x >> 2), (float*)s_lds + RT_QSTACK * 64 + (threadIdx.x >> 2)};
         if (closest)
-            trace_stream<false, STATS, PAIR, 4>(W, S, stk, s_pre, c0, total, wg, wn, fbn, fbl, ps);
+            trace_stream<false, STATS, PAIR, 4>(W, S, stk, s_pre, c0, total, wg, wn, fbn, fbl, ps, pf);
         else
-            trace_stream<true, STATS, PAIR, 4>(W, S, stk, s_pre, a0, total, wg, wn, fbn, fbl, ps);
+            trace_stream<true, STATS, PAIR, 4>(W, S, stk, s_pre, a0, total, wg, wn, fbn, fbl, ps, pf);
     } else {
         static_assert(2 * RT_RSTACK * 16 <= RT_LDS_WORDS * 256, "row stacks fit k_trace's LDS");
         rtk::QuadStack<RT_RSTACK, 16> stk{s_lds + (threadIdx.x >> 4), (float*)s_lds + RT_RSTACK * 16 + (threadIdx.x >> 4)};
         if (closest)
-            trace_stream<false, STATS, PAIR, 16>(W, S, stk, s_pre, c0, total, wg, wn, fbn, fbl, ps);
+            trace_stream<false, STATS, PAIR, 16>(W, S, stk, s_pre, c0, total, wg, wn, fbn, fbl, ps, pf);
         else
-            trace_stream<true, STATS, PAIR, 16>(W, S, stk, s_pre, a0, total, wg, wn, fbn, fbl, ps);
+            trace_stream<true, STATS, PAIR, 16>(W, S, stk, s_pre, a0, total, wg, wn, fbn, fbl, ps, pf);
     }
     flush_stats<STATS>(st, stats);
 }
